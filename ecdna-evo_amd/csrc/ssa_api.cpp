@@ -1,0 +1,457 @@
+// ssa_api.cpp — the C ABI of include/ecdna_ssa.h: parameter validation,
+// device-resident run contexts, chunking by HBM capacity, and launches of the
+// stepper and histogram kernels (ssa_kernels.hip).
+//
+// This file replaces, for one GPU, the per-replicate driver loop of the
+// reference: run_simulations(idx) mapped by rayon over seed*10 .. seed*10+runs
+// (src/main.rs:55-225). Everything here is host code; there is no CPU
+// fallback — without a gfx950 device every entry point returns
+// ECDNA_E_NODEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ecdna_ssa.h"
+#include "ssa_launch.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                                \
+    do {                                                                                             \
+        hipError_t _e = (expr);                                                                      \
+        if (_e != hipSuccess)                                                                        \
+            return fail(_e == hipErrorOutOfMemory ? ECDNA_E_NOMEM : ECDNA_E_HIP,                     \
+                        std::string(#expr) + ": " + hipGetErrorString(_e));                          \
+    } while (0)
+
+uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
+
+struct InitOfSet {
+    const uint16_t* copies;
+    uint64_t nplus;
+    uint64_t nminus;
+};
+
+InitOfSet init_of_set(const ecdna_ssa_params_t* p, uint64_t s) {
+    InitOfSet r;
+    if (p->init_set_offsets) {
+        r.copies = p->init_copies + p->init_set_offsets[s];
+        r.nplus = p->init_set_offsets[s + 1] - p->init_set_offsets[s];
+    } else {
+        r.copies = p->init_copies;
+        r.nplus = p->init_nplus;
+    }
+    r.nminus = p->init_set_nminus ? p->init_set_nminus[s] : p->init_nminus;
+    return r;
+}
+
+int validate(const ecdna_ssa_params_t* p) {
+    if (!p) return fail(ECDNA_E_INVALID, "params is NULL");
+    if (!p->rates || p->n_param_sets == 0) return fail(ECDNA_E_INVALID, "rates/n_param_sets");
+    if (p->reps_per_set == 0) return fail(ECDNA_E_INVALID, "reps_per_set must be >= 1");
+    if (p->hist_bins < 2 || p->hist_bins > ecdna::kMaxHistBins)
+        return fail(ECDNA_E_INVALID, "hist_bins must be in [2, 4096]");
+    if (p->process != ECDNA_PURE_BIRTH && p->process != ECDNA_BIRTH_DEATH)
+        return fail(ECDNA_E_INVALID, "unknown process");
+    if (p->segregation < 0 || p->segregation > 3) return fail(ECDNA_E_INVALID, "unknown segregation");
+    if (p->max_iter > 0xffffffffull) return fail(ECDNA_E_INVALID, "max_iter must be < 2^32");
+    if (p->n_replicates > 0xffffffffull) return fail(ECDNA_E_INVALID, "n_replicates must be < 2^32 per call");
+    if (p->n_replicates && (p->first_replicate + p->n_replicates - 1) / p->reps_per_set >= p->n_param_sets)
+        return fail(ECDNA_E_INVALID, "replicate ids map past the last parameter set");
+    if (p->cell_cap == 0) return fail(ECDNA_E_INVALID, "cell_cap must be >= 1");
+    if (!p->init_copies && (p->init_nplus || p->init_set_offsets))
+        return fail(ECDNA_E_INVALID, "init_copies is NULL");
+    for (uint32_t s = 0; s < p->n_param_sets; ++s) {
+        InitOfSet in = init_of_set(p, s);
+        if (in.nplus > p->cell_cap) return fail(ECDNA_E_INVALID, "initial N+ cells exceed cell_cap");
+        if (in.nminus > 0xffffffffull) return fail(ECDNA_E_INVALID, "initial N- cells must be < 2^32");
+        for (uint64_t j = 0; j < in.nplus; ++j)
+            if (in.copies[j] == 0) return fail(ECDNA_E_INVALID, "initial copy numbers must be >= 1");
+        if (!p->init_set_offsets && !p->init_set_nminus) break;
+    }
+    return ECDNA_OK;
+}
+
+struct Chunk {
+    uint64_t first;  // local index of the first replicate
+    uint32_t n;
+    hipEvent_t ev[3];
+};
+
+}  // namespace
+
+struct ecdna_ssa_ctx {
+    ecdna_ssa_params_t p{};
+    int device = 0;
+    int cus = 0;
+    uint64_t row_stride = 0;
+    uint64_t chunk_reps = 0;
+    uint32_t stepper_blocks_cap = 0;
+    // owned copies of the host inputs
+    std::vector<ecdna_rates_t> rates;
+    std::vector<uint16_t> init_copies;
+    std::vector<uint32_t> init_offsets;
+    std::vector<uint64_t> init_nminus_set;
+    // device buffers
+    float4* d_rates = nullptr;
+    uint16_t* d_init = nullptr;
+    uint32_t* d_init_off = nullptr;
+    uint64_t* d_init_nm = nullptr;
+    uint16_t* d_rows = nullptr;
+    ecdna_rep_summary_t* d_summ = nullptr;
+    uint32_t* d_heads = nullptr;  // one work counter per chunk
+    uint64_t* d_hist_own = nullptr;
+    ecdna_totals_t* d_tot_own = nullptr;
+    uint64_t* d_hist = nullptr;
+    ecdna_totals_t* d_tot = nullptr;
+    hipStream_t own_stream = nullptr;
+    hipStream_t last_stream = nullptr;
+    std::vector<Chunk> chunks;
+    bool launched = false;
+};
+
+namespace {
+
+int pick_device(int dev) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(ECDNA_E_NODEVICE, "no HIP device");
+    if (dev < 0 || dev >= n) return fail(ECDNA_E_NODEVICE, "device ordinal out of range");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return fail(ECDNA_E_NODEVICE, "device query failed");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(ECDNA_E_NODEVICE, std::string("not a gfx950 device: ") + prop.gcnArchName);
+    if (hipSetDevice(dev) != hipSuccess) return fail(ECDNA_E_NODEVICE, "hipSetDevice failed");
+    return ECDNA_OK;
+}
+
+uint64_t env_u64(const char* name, uint64_t dflt) {
+    const char* v = std::getenv(name);
+    if (!v || !*v) return dflt;
+    return std::strtoull(v, nullptr, 10);
+}
+
+void free_ctx(ecdna_ssa_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    for (auto& ch : c->chunks)
+        for (auto& e : ch.ev)
+            if (e) (void)hipEventDestroy(e);
+    (void)hipFree(c->d_rates);
+    (void)hipFree(c->d_init);
+    (void)hipFree(c->d_init_off);
+    (void)hipFree(c->d_init_nm);
+    (void)hipFree(c->d_rows);
+    (void)hipFree(c->d_summ);
+    (void)hipFree(c->d_heads);
+    (void)hipFree(c->d_hist_own);
+    (void)hipFree(c->d_tot_own);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ecdna_ssa_abi_version(void) { return ECDNA_SSA_ABI_VERSION; }
+
+const char* ecdna_ssa_strerror(int code) {
+    switch (code) {
+        case ECDNA_OK: return "ok";
+        case ECDNA_E_INVALID: return "invalid argument";
+        case ECDNA_E_HIP: return "HIP runtime error";
+        case ECDNA_E_NOMEM: return "device out of memory";
+        case ECDNA_E_NODEVICE: return "no usable gfx950 device";
+        case ECDNA_E_STATE: return "invalid call order";
+        default: return "unknown error";
+    }
+}
+
+const char* ecdna_ssa_last_error_message(void) { return g_last_error.c_str(); }
+
+int ecdna_ssa_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    int good = 0;
+    for (int d = 0; d < n; ++d) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0)
+            ++good;
+    }
+    return good;
+}
+
+int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
+    if (!out) return fail(ECDNA_E_INVALID, "out is NULL");
+    *out = nullptr;
+    int rc = validate(p);
+    if (rc) return rc;
+    rc = pick_device(p->device);
+    if (rc) return rc;
+
+    ecdna_ssa_ctx* c = new ecdna_ssa_ctx();
+    c->p = *p;
+    c->device = p->device;
+    // own copies of host inputs
+    c->rates.assign(p->rates, p->rates + p->n_param_sets);
+    uint64_t n_init = p->init_set_offsets ? p->init_set_offsets[p->n_param_sets] : p->init_nplus;
+    c->init_copies.assign(p->init_copies ? p->init_copies : nullptr,
+                          p->init_copies ? p->init_copies + n_init : nullptr);
+    if (c->init_copies.empty()) c->init_copies.push_back(1);
+    if (p->init_set_offsets) c->init_offsets.assign(p->init_set_offsets, p->init_set_offsets + p->n_param_sets + 1);
+    if (p->init_set_nminus) c->init_nminus_set.assign(p->init_set_nminus, p->init_set_nminus + p->n_param_sets);
+    c->p.rates = nullptr;
+    c->p.init_copies = nullptr;
+    c->p.init_set_offsets = nullptr;
+    c->p.init_set_nminus = nullptr;
+
+    auto bail = [&](int code) {
+        free_ctx(c);
+        return code;
+    };
+#define CTX_TRY(expr)                                                                                \
+    do {                                                                                             \
+        hipError_t _e = (expr);                                                                      \
+        if (_e != hipSuccess)                                                                        \
+            return bail(fail(_e == hipErrorOutOfMemory ? ECDNA_E_NOMEM : ECDNA_E_HIP,                \
+                             std::string(#expr) + ": " + hipGetErrorString(_e)));                     \
+    } while (0)
+
+    hipDeviceProp_t prop;
+    CTX_TRY(hipGetDeviceProperties(&prop, c->device));
+    c->cus = prop.multiProcessorCount;
+    CTX_TRY(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+
+    // inputs
+    std::vector<float4> r4(p->n_param_sets);
+    for (uint32_t s = 0; s < p->n_param_sets; ++s)
+        r4[s] = make_float4(p->rates[s].b0, p->rates[s].b1, p->rates[s].d0, p->rates[s].d1);
+    CTX_TRY(hipMalloc(&c->d_rates, r4.size() * sizeof(float4)));
+    CTX_TRY(hipMemcpy(c->d_rates, r4.data(), r4.size() * sizeof(float4), hipMemcpyHostToDevice));
+    CTX_TRY(hipMalloc(&c->d_init, c->init_copies.size() * sizeof(uint16_t)));
+    CTX_TRY(hipMemcpy(c->d_init, c->init_copies.data(), c->init_copies.size() * sizeof(uint16_t),
+                      hipMemcpyHostToDevice));
+    if (!c->init_offsets.empty()) {
+        CTX_TRY(hipMalloc(&c->d_init_off, c->init_offsets.size() * sizeof(uint32_t)));
+        CTX_TRY(hipMemcpy(c->d_init_off, c->init_offsets.data(), c->init_offsets.size() * sizeof(uint32_t),
+                          hipMemcpyHostToDevice));
+    }
+    if (!c->init_nminus_set.empty()) {
+        CTX_TRY(hipMalloc(&c->d_init_nm, c->init_nminus_set.size() * sizeof(uint64_t)));
+        CTX_TRY(hipMemcpy(c->d_init_nm, c->init_nminus_set.data(), c->init_nminus_set.size() * sizeof(uint64_t),
+                          hipMemcpyHostToDevice));
+    }
+
+    // outputs
+    const uint64_t n = p->n_replicates;
+    const uint64_t nb = (uint64_t)p->n_param_sets * p->hist_bins;
+    CTX_TRY(hipMalloc(&c->d_hist_own, nb * sizeof(uint64_t)));
+    CTX_TRY(hipMalloc(&c->d_tot_own, p->n_param_sets * sizeof(ecdna_totals_t)));
+    CTX_TRY(hipMemset(c->d_hist_own, 0, nb * sizeof(uint64_t)));
+    CTX_TRY(hipMemset(c->d_tot_own, 0, p->n_param_sets * sizeof(ecdna_totals_t)));
+    c->d_hist = c->d_hist_own;
+    c->d_tot = c->d_tot_own;
+    CTX_TRY(hipMalloc(&c->d_summ, std::max<uint64_t>(n, 1) * sizeof(ecdna_rep_summary_t)));
+
+    // rows: one u16 row per replicate of the chunk; chunk bounded by free HBM
+    c->row_stride = round_up(p->cell_cap, 64);
+    const uint64_t row_bytes = c->row_stride * sizeof(uint16_t);
+    size_t free_b = 0, total_b = 0;
+    CTX_TRY(hipMemGetInfo(&free_b, &total_b));
+    uint64_t budget = (uint64_t)((double)free_b * 0.85);
+    uint64_t cap_budget = env_u64("ECDNA_SSA_MAX_ROW_BYTES", 0);
+    if (cap_budget) budget = std::min<uint64_t>(budget, cap_budget);
+    uint64_t fit = budget / row_bytes;
+    uint64_t max_chunk = env_u64("ECDNA_SSA_MAX_CHUNK", 0);
+    if (max_chunk) fit = std::min<uint64_t>(fit, max_chunk);
+    if (fit == 0) return bail(fail(ECDNA_E_NOMEM, "one replicate row does not fit in device memory"));
+    c->chunk_reps = std::min<uint64_t>(std::max<uint64_t>(n, 1), fit);
+    CTX_TRY(hipMalloc(&c->d_rows, c->chunk_reps * row_bytes));
+
+    const uint64_t n_chunks = n ? (n + c->chunk_reps - 1) / c->chunk_reps : 0;
+    CTX_TRY(hipMalloc(&c->d_heads, std::max<uint64_t>(n_chunks, 1) * sizeof(uint32_t)));
+    for (uint64_t k = 0; k < n_chunks; ++k) {
+        Chunk ch{};
+        ch.first = k * c->chunk_reps;
+        ch.n = (uint32_t)std::min<uint64_t>(c->chunk_reps, n - ch.first);
+        c->chunks.push_back(ch);
+        for (auto& e : c->chunks.back().ev) CTX_TRY(hipEventCreate(&e));
+    }
+
+    // persistent stepper grid: as many resident lanes as the occupancy allows
+    int per_cu = 0;
+    CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ecdna::stepper_kernel(p->process, p->segregation),
+                                                         ecdna::kStepperBlock, 0));
+    uint64_t bpc = env_u64("ECDNA_SSA_BLOCKS_PER_CU", 0);
+    if (bpc) per_cu = (int)bpc;
+    if (per_cu < 1) per_cu = 1;
+    c->stepper_blocks_cap = (uint32_t)(per_cu * c->cus);
+    uint64_t max_blocks = env_u64("ECDNA_SSA_MAX_BLOCKS", 0);  // testing: force lane refill
+    if (max_blocks) c->stepper_blocks_cap = (uint32_t)std::min<uint64_t>(c->stepper_blocks_cap, max_blocks);
+    *out = c;
+    return ECDNA_OK;
+#undef CTX_TRY
+}
+
+int ecdna_ssa_ctx_set_outputs(ecdna_ssa_ctx* c, uint64_t* d_hist, ecdna_totals_t* d_totals) {
+    if (!c) return fail(ECDNA_E_INVALID, "ctx is NULL");
+    c->d_hist = d_hist ? d_hist : c->d_hist_own;
+    c->d_tot = d_totals ? d_totals : c->d_tot_own;
+    return ECDNA_OK;
+}
+
+int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
+    if (!c) return fail(ECDNA_E_INVALID, "ctx is NULL");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->own_stream;
+    const ecdna_ssa_params_t& p = c->p;
+    const uint64_t nb = (uint64_t)p.n_param_sets * p.hist_bins;
+    HIP_TRY(hipMemsetAsync(c->d_hist, 0, nb * sizeof(uint64_t), st));
+    HIP_TRY(hipMemsetAsync(c->d_tot, 0, p.n_param_sets * sizeof(ecdna_totals_t), st));
+    if (!c->chunks.empty())
+        HIP_TRY(hipMemsetAsync(c->d_heads, 0, c->chunks.size() * sizeof(uint32_t), st));
+
+    for (size_t k = 0; k < c->chunks.size(); ++k) {
+        Chunk& ch = c->chunks[k];
+        ecdna::StepperArgs a{};
+        a.rows = c->d_rows;
+        a.summaries = c->d_summ + ch.first;
+        a.head = c->d_heads + k;
+        a.rates = c->d_rates;
+        a.init_copies = c->d_init;
+        a.init_offsets = c->d_init_off;
+        a.init_nminus_set = c->d_init_nm;
+        a.row_stride = c->row_stride;
+        a.seed = p.seed;
+        a.rid0 = p.first_replicate + ch.first;
+        a.reps_per_set = p.reps_per_set;
+        a.max_cells = p.max_cells;
+        a.init_nminus = p.init_nminus;
+        a.max_time = p.max_time;
+        a.max_time32 = (float)p.max_time;
+        a.n = ch.n;
+        a.init_nplus = p.init_nplus;
+        a.max_iter = (uint32_t)p.max_iter;
+        a.cell_cap = p.cell_cap;
+        a.flags = p.flags;
+        a.cells_mul = (p.process == ECDNA_BIRTH_DEATH && (p.flags & ECDNA_FLAG_BD_CAP_COMPAT)) ? 2u : 1u;
+        const uint32_t need = (ch.n + ecdna::kStepperBlock - 1) / ecdna::kStepperBlock;
+        const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(need, c->stepper_blocks_cap));
+
+        HIP_TRY(hipEventRecord(ch.ev[0], st));
+        HIP_TRY(ecdna::launch_stepper(a, p.process, p.segregation, blocks, st));
+        HIP_TRY(hipEventRecord(ch.ev[1], st));
+
+        ecdna::HistArgs hsa{};
+        hsa.rows = c->d_rows;
+        hsa.summaries = c->d_summ + ch.first;
+        hsa.hist = c->d_hist;
+        hsa.totals = reinterpret_cast<unsigned long long*>(c->d_tot);
+        hsa.row_stride = c->row_stride;
+        hsa.rid0 = p.first_replicate + ch.first;
+        hsa.reps_per_set = p.reps_per_set;
+        hsa.n = ch.n;
+        hsa.bins = p.hist_bins;
+        const uint32_t hist_blocks_max = (uint32_t)c->cus * 8u;
+        uint32_t rpb = (ch.n + hist_blocks_max - 1) / hist_blocks_max;
+        if (rpb < 4) rpb = 4;
+        hsa.reps_per_block = rpb;
+        const uint32_t hblocks = (ch.n + rpb - 1) / rpb;
+        HIP_TRY(ecdna::launch_hist(hsa, hblocks, st));
+        HIP_TRY(hipEventRecord(ch.ev[2], st));
+    }
+    c->last_stream = st;
+    c->launched = true;
+    return ECDNA_OK;
+}
+
+int ecdna_ssa_ctx_sync(ecdna_ssa_ctx* c, float* ssa_ms, float* hist_ms) {
+    if (!c) return fail(ECDNA_E_INVALID, "ctx is NULL");
+    if (!c->launched) return fail(ECDNA_E_STATE, "sync before launch");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->last_stream));
+    float s = 0.f, h = 0.f;
+    for (auto& ch : c->chunks) {
+        float a = 0.f, b = 0.f;
+        HIP_TRY(hipEventElapsedTime(&a, ch.ev[0], ch.ev[1]));
+        HIP_TRY(hipEventElapsedTime(&b, ch.ev[1], ch.ev[2]));
+        s += a;
+        h += b;
+    }
+    if (ssa_ms) *ssa_ms = s;
+    if (hist_ms) *hist_ms = h;
+    return ECDNA_OK;
+}
+
+int ecdna_ssa_ctx_device_outputs(ecdna_ssa_ctx* c, uint64_t** d_hist, ecdna_totals_t** d_totals) {
+    if (!c) return fail(ECDNA_E_INVALID, "ctx is NULL");
+    if (d_hist) *d_hist = c->d_hist;
+    if (d_totals) *d_totals = c->d_tot;
+    return ECDNA_OK;
+}
+
+int64_t ecdna_ssa_ctx_row_stride(const ecdna_ssa_ctx* c) {
+    if (!c) return 0;
+    return c->chunks.size() <= 1 ? (int64_t)c->row_stride : 0;
+}
+
+int ecdna_ssa_ctx_geometry(const ecdna_ssa_ctx* c, uint64_t* chunk_replicates, uint64_t* grid_lanes) {
+    if (!c) return fail(ECDNA_E_INVALID, "ctx is NULL");
+    if (chunk_replicates) *chunk_replicates = c->chunk_reps;
+    if (grid_lanes) *grid_lanes = (uint64_t)c->stepper_blocks_cap * ecdna::kStepperBlock;
+    return ECDNA_OK;
+}
+
+int ecdna_ssa_ctx_download(ecdna_ssa_ctx* c, ecdna_rep_summary_t* out_summaries, uint64_t* out_hist,
+                           ecdna_totals_t* out_totals, uint16_t* out_rows) {
+    if (!c) return fail(ECDNA_E_INVALID, "ctx is NULL");
+    if (!c->launched) return fail(ECDNA_E_STATE, "download before launch");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->last_stream));
+    const ecdna_ssa_params_t& p = c->p;
+    if (out_summaries && p.n_replicates)
+        HIP_TRY(hipMemcpy(out_summaries, c->d_summ, p.n_replicates * sizeof(ecdna_rep_summary_t),
+                          hipMemcpyDeviceToHost));
+    if (out_hist)
+        HIP_TRY(hipMemcpy(out_hist, c->d_hist, (uint64_t)p.n_param_sets * p.hist_bins * sizeof(uint64_t),
+                          hipMemcpyDeviceToHost));
+    if (out_totals)
+        HIP_TRY(hipMemcpy(out_totals, c->d_tot, p.n_param_sets * sizeof(ecdna_totals_t), hipMemcpyDeviceToHost));
+    if (out_rows) {
+        if (c->chunks.size() > 1) return fail(ECDNA_E_STATE, "rows are not downloadable from a chunked run");
+        if (p.n_replicates)
+            HIP_TRY(hipMemcpy(out_rows, c->d_rows, p.n_replicates * c->row_stride * sizeof(uint16_t),
+                              hipMemcpyDeviceToHost));
+    }
+    return ECDNA_OK;
+}
+
+int ecdna_ssa_ctx_destroy(ecdna_ssa_ctx* c) {
+    free_ctx(c);
+    return ECDNA_OK;
+}
+
+int ecdna_ssa_run(const ecdna_ssa_params_t* p, ecdna_rep_summary_t* out_summaries, uint64_t* out_hist,
+                  ecdna_totals_t* out_totals, void* stream) {
+    ecdna_ssa_ctx* c = nullptr;
+    int rc = ecdna_ssa_ctx_create(p, &c);
+    if (rc) return rc;
+    rc = ecdna_ssa_ctx_launch(c, stream);
+    if (!rc) rc = ecdna_ssa_ctx_download(c, out_summaries, out_hist, out_totals, nullptr);
+    ecdna_ssa_ctx_destroy(c);
+    return rc;
+}
+
+}  // extern "C"

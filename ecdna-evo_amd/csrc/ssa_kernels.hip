@@ -1,0 +1,353 @@
+// ssa_kernels.hip — the MI355X (gfx950) many-replicate Gillespie SSA stepper
+// and the copy-number histogram pass.
+//
+// One replicate per lane. A lane runs the whole sosa::simulate loop
+// (external crate sosa 3.0.3; call sites src/main.rs:92-99, 166-173) for its
+// replicate: stop checks, propensities of update_state's population vector
+// (src/process.rs:187-196, 339-344), one Philox4x32-10 block per event, the
+// direct-method channel pick, the event of advance_step
+// (src/process.rs:147-184, 291-336) — Exponential::increase_nplus with its
+// swap_remove pick and Segregate rule (src/proliferation.rs:25-111,
+// src/segregation.rs:110-194), increase_nminus / CellDeath
+// (src/proliferation.rs:113-140) — and the time accumulation
+// (src/process.rs:184, 336). When its replicate stops, the lane writes the
+// summary and pulls the next replicate id from a work counter (persistent
+// grid), so early extinctions in birth–death runs do not idle the lane.
+//
+// Memory: every replicate owns a u16 row of row_stride cells in HBM
+// (replicate-major, 128-B aligned). An event touches at most one random cell
+// (the swap_remove pick) plus the row's tail; the tail VALUE is cached in a
+// register (the reference re-reads it through Vec::swap_remove), so a
+// ProliferateNPlus costs one random 2-B load and up to three 2-B stores.
+#include "ssa_device.hpp"
+#include "ssa_launch.h"
+
+#pragma clang fp contract(off)
+
+namespace ecdna {
+
+constexpr uint64_t kFnvOffset = 0xcbf29ce484222325ull;
+constexpr uint64_t kFnvPrime = 0x100000001b3ull;
+constexpr uint32_t kNoUnevenMaxTries = 4096;
+
+template <bool BD, int SEG>
+__global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a) {
+    const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+    const bool f32t = (a.flags & ECDNA_FLAG_TIME_F32) != 0;
+    const bool hash_on = (a.flags & ECDNA_FLAG_EVENT_HASH) != 0;
+
+    bool active = false, have = false;
+    uint32_t li = 0;
+    uint64_t rid = 0;
+    uint16_t* row = nullptr;
+    uint32_t nm = 0, np = 0, tail = 0;
+    bool tail_ok = false;
+    float b0 = 0.f, b1 = 0.f, d0 = 0.f, d1 = 0.f;
+    double t = 0.0;
+    float t32 = 0.f;
+    uint32_t e = 0, n_pm = 0, n_pp = 0, n_dm = 0, n_dp = 0, n_un = 0;
+    uint64_t h = kFnvOffset;
+    uint32_t stop = 0, err = 0;
+
+    for (;;) {
+        if (!active) {
+            if (have) {
+                ecdna_rep_summary_t* s = a.summaries + li;
+                s->nminus = nm;
+                s->nplus = np;
+                s->iters = e;
+                s->events_by_type[0] = n_pm;
+                s->events_by_type[1] = n_pp;
+                s->events_by_type[2] = n_dm;
+                s->events_by_type[3] = n_dp;
+                s->uneven = n_un;
+                s->time = f32t ? (double)t32 : t;
+                s->event_hash = hash_on ? h : 0ull;
+                s->stop_reason = stop;
+                s->error = err;
+            }
+            const uint32_t i = atomicAdd(a.head, 1u);
+            if (i >= a.n) break;
+            have = true;
+            active = true;
+            li = i;
+            rid = a.rid0 + i;
+            row = a.rows + (uint64_t)i * a.row_stride;
+            const uint64_t set = rid / a.reps_per_set;
+            const float4 r = a.rates[set];
+            b0 = r.x;
+            b1 = r.y;
+            d0 = r.z;
+            d1 = r.w;
+            const uint16_t* src = a.init_copies;
+            uint32_t cnt = a.init_nplus;
+            if (a.init_offsets) {
+                src = a.init_copies + a.init_offsets[set];
+                cnt = a.init_offsets[set + 1] - a.init_offsets[set];
+            }
+            for (uint32_t j = 0; j < cnt; ++j) row[j] = src[j];
+            np = cnt;
+            nm = (uint32_t)(a.init_nminus_set ? a.init_nminus_set[set] : a.init_nminus);
+            tail_ok = false;
+            t = 0.0;
+            t32 = 0.f;
+            e = n_pm = n_pp = n_dm = n_dp = n_un = 0;
+            h = kFnvOffset;
+            stop = 0;
+            err = 0;
+            if (np == 0 && nm == 0) {  // ensure!(!distribution.is_empty()) src/process.rs:88, 232
+                err = ECDNA_REP_ERR_EMPTY;
+                stop = ECDNA_STOP_ERROR;
+                active = false;
+                continue;
+            }
+        }
+
+        // propensities rate_i * population_i over [n-, n+(, n-, n+)]
+        const double pa = (double)b0 * (double)nm;
+        const double pb = (double)b1 * (double)np;
+        const double cA = pa;
+        const double cB = cA + pb;
+        double cC = cB, a0 = cB;
+        if (BD) {
+            const double pc = (double)d0 * (double)nm;
+            const double pd = (double)d1 * (double)np;
+            cC = cB + pc;
+            a0 = cC + pd;
+        }
+
+        // stop checks, in the order of DESIGN.md §3.1
+        {
+            const uint64_t cells = ((uint64_t)nm + np) * a.cells_mul;
+            uint32_t s = 0;
+            if (e >= a.max_iter)
+                s = ECDNA_STOP_MAX_ITER;
+            else if (cells >= a.max_cells)
+                s = ECDNA_STOP_MAX_CELLS;
+            else if (f32t ? (t32 >= a.max_time32) : (t >= a.max_time))
+                s = ECDNA_STOP_MAX_TIME;
+            else if (!(a0 > 0.0))
+                s = ECDNA_STOP_ABSORBING;
+            if (s) {
+                stop = s;
+                active = false;
+                continue;
+            }
+        }
+
+        if (!tail_ok && np > 0) {  // refill the cached tail value (after a DeathNPlus)
+            tail = row[np - 1];
+            tail_ok = true;
+        }
+
+        const uint32_t rid_lo = (uint32_t)rid, rid_hi = (uint32_t)(rid >> 32);
+        const uint4 w = philox4x32_10(make_uint4(e, 0u, rid_lo, rid_hi), k0, k1);
+        const double target = (((double)w.y + 0.5) * 0x1p-32) * a0;
+        uint32_t ch;
+        if (BD)
+            ch = target < cA ? 0u : (target < cB ? 1u : (target < cC ? 2u : 3u));
+        else
+            ch = target < cA ? 0u : 1u;
+
+        WordStream ws;
+        ws.w2 = w.z;
+        ws.w3 = w.w;
+        ws.e = e;
+        ws.rid_lo = rid_lo;
+        ws.rid_hi = rid_hi;
+        ws.k0 = k0;
+        ws.k1 = k1;
+        ws.pos = 1;
+        ws.blk_id = 0;
+        ws.blk = make_uint4(0, 0, 0, 0);
+
+        uint32_t idx = 0, k = 0;
+        if (ch & 1u) {
+            // uniform N+ cell: Lemire multiply-shift on w2, exact rejection from the stream
+            uint64_t m = (uint64_t)w.z * np;
+            uint32_t lo = (uint32_t)m;
+            if (lo < np) {
+                const uint32_t thr = (0u - np) % np;
+                while (lo < thr) {
+                    m = (uint64_t)ws.next() * np;
+                    lo = (uint32_t)m;
+                }
+            }
+            idx = (uint32_t)(m >> 32);
+            if (ch == 1u) k = (idx == np - 1) ? tail : (uint32_t)row[idx];
+        }
+
+        // waiting time: independent of the load above, hides its latency
+        const double tau = softlog_neg(w.x) / a0;
+
+        uint64_t x = ch;
+        if (ch == 1u) {  // Exponential::increase_nplus (src/proliferation.rs:25-111)
+            if (k > 32767u) {  // checked_mul panic (src/proliferation.rs:63-67)
+                err = ECDNA_REP_ERR_OVERFLOW;
+                stop = ECDNA_STOP_ERROR;
+                active = false;
+                continue;
+            }
+            const uint32_t n = 2u * k;
+            uint32_t k1v;
+            uint32_t un = 0;  // 0 False, 1 True, 2 TrueWithoutNMinusIncrease
+            if (SEG == ECDNA_SEG_DETERMINISTIC) {
+                k1v = k;
+            } else {
+                if (ws.pos == 1 && n <= 32u) {
+                    k1v = __popc(n == 32u ? w.w : (w.w & ((1u << n) - 1u)));
+                    ws.pos = 2;
+                } else {
+                    k1v = ws.binomial_half(n);
+                }
+                if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN) {
+                    uint32_t tries = 1;
+                    bool rej = false;
+                    while (k1v == 0u || k1v == n) {
+                        if (tries == kNoUnevenMaxTries) {
+                            rej = true;
+                            break;
+                        }
+                        k1v = ws.binomial_half(n);
+                        ++tries;
+                    }
+                    if (rej) {
+                        err = ECDNA_REP_ERR_REJECTION;
+                        stop = ECDNA_STOP_ERROR;
+                        active = false;
+                        continue;
+                    }
+                } else if (k1v == 0u || k1v == n) {
+                    un = (SEG == ECDNA_SEG_BINOMIAL_NO_NMINUS) ? 2u : 1u;
+                }
+            }
+            if (un == 0u && np + 1u > a.cell_cap) {
+                err = ECDNA_REP_ERR_CELL_CAP;
+                stop = ECDNA_STOP_ERROR;
+                active = false;
+                continue;
+            }
+            if (idx != np - 1) row[idx] = (uint16_t)tail;  // swap_remove(idx)
+            if (un == 0u) {
+                row[np - 1] = (uint16_t)k1v;  // push k1, push k2
+                row[np] = (uint16_t)(n - k1v);
+                np += 1;
+                tail = n - k1v;
+            } else {
+                row[np - 1] = (uint16_t)n;  // push k1 + k2
+                tail = n;
+                if (un == 1u) nm += 1;
+                n_un += 1;
+            }
+            x |= ((uint64_t)k1v << 2) | ((uint64_t)idx << 20);
+            n_pp += 1;
+        } else if (BD && ch == 3u) {  // CellDeath::decrease_nplus (src/proliferation.rs:126-133)
+            if (idx != np - 1) row[idx] = (uint16_t)tail;
+            np -= 1;
+            tail_ok = (np > 0) && (idx == np - 1);
+            x |= (uint64_t)idx << 20;
+            n_dp += 1;
+        } else if (ch == 0u) {  // increase_nminus (src/proliferation.rs:113-117)
+            nm += 1;
+            n_pm += 1;
+        } else {  // decrease_nminus (src/proliferation.rs:135-139)
+            nm -= 1;
+            n_dm += 1;
+        }
+        e += 1;
+        if (f32t)
+            t32 = t32 + (float)tau;
+        else
+            t = t + tau;
+        if (hash_on) h = (h ^ x) * kFnvPrime;
+    }
+}
+
+// Histogram + totals over one chunk. Each workgroup owns a contiguous range of replicates; per
+// parameter set it accumulates in LDS (u64 atomics) and flushes non-zero bins with one global
+// atomic each. Rows are read 16 B (8 cells) per lane per load.
+__global__ void __launch_bounds__(kHistBlock) ssa_hist(const HistArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long lds[];
+    unsigned long long* hb = lds;                // [bins]
+    unsigned long long* tb = lds + a.bins;       // [16] totals words
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t nw = blockDim.x >> 6;
+    const uint32_t r_begin = blockIdx.x * a.reps_per_block;
+    if (r_begin >= a.n) return;
+    const uint32_t r_end = min(a.n, r_begin + a.reps_per_block);
+    const uint32_t last = a.bins - 1;
+
+    uint32_t r = r_begin;
+    while (r < r_end) {
+        const uint64_t set = (a.rid0 + r) / a.reps_per_set;
+        const uint64_t set_end_rid = (set + 1) * a.reps_per_set;
+        const uint32_t seg_end = (uint32_t)min((uint64_t)r_end, set_end_rid - a.rid0);
+        for (uint32_t b = tid; b < a.bins + 16; b += blockDim.x) lds[b] = 0ull;
+        __syncthreads();
+        for (uint32_t q = r + wave; q < seg_end; q += nw) {
+            const ecdna_rep_summary_t* s = a.summaries + q;
+            const uint32_t np = (uint32_t)s->nplus;
+            const uint16_t* row = a.rows + (uint64_t)q * a.row_stride;
+            for (uint32_t c = lane * 8u; c < np; c += 512u) {
+                const uint4 v = *reinterpret_cast<const uint4*>(row + c);
+                const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    if (c + (uint32_t)j < np) {
+                        const uint32_t kk = (wv[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
+                        atomicAdd(&hb[kk < last ? kk : last], 1ull);
+                    }
+                }
+            }
+            if (lane == 0) {
+                atomicAdd(&hb[0], (unsigned long long)s->nminus);
+                atomicAdd(&tb[0], 1ull);
+                atomicAdd(&tb[1], (unsigned long long)s->iters);
+                atomicAdd(&tb[2], (unsigned long long)s->events_by_type[0]);
+                atomicAdd(&tb[3], (unsigned long long)s->events_by_type[1]);
+                atomicAdd(&tb[4], (unsigned long long)s->events_by_type[2]);
+                atomicAdd(&tb[5], (unsigned long long)s->events_by_type[3]);
+                atomicAdd(&tb[6], (unsigned long long)s->uneven);
+                atomicAdd(&tb[7], (unsigned long long)s->nminus);
+                atomicAdd(&tb[8], (unsigned long long)s->nplus);
+                atomicAdd(&tb[9 + (s->stop_reason < 6u ? s->stop_reason : 5u)], 1ull);
+                if (s->error) atomicAdd(&tb[15], 1ull);
+            }
+        }
+        __syncthreads();
+        for (uint32_t b = tid; b < a.bins; b += blockDim.x)
+            if (hb[b]) atomicAdd((unsigned long long*)&a.hist[set * a.bins + b], hb[b]);
+        if (tid < 16 && tb[tid]) atomicAdd(&a.totals[set * 16 + tid], tb[tid]);
+        __syncthreads();
+        r = seg_end;
+    }
+}
+
+// ---------------------------------------------------------------- launch
+
+#define ECDNA_STEPPER_TABLE(BD) \
+    {(const void*)ssa_stepper<BD, 0>, (const void*)ssa_stepper<BD, 1>, (const void*)ssa_stepper<BD, 2>, \
+     (const void*)ssa_stepper<BD, 3>}
+
+static const void* const kStepperTable[2][4] = {ECDNA_STEPPER_TABLE(false), ECDNA_STEPPER_TABLE(true)};
+
+const void* stepper_kernel(int birth_death, int segregation) {
+    return kStepperTable[birth_death ? 1 : 0][segregation & 3];
+}
+
+hipError_t launch_stepper(const StepperArgs& a, int birth_death, int segregation, uint32_t blocks,
+                          hipStream_t stream) {
+    StepperArgs copy = a;
+    void* args[] = {&copy};
+    return hipLaunchKernel(stepper_kernel(birth_death, segregation), dim3(blocks), dim3(kStepperBlock), args, 0,
+                           stream);
+}
+
+hipError_t launch_hist(const HistArgs& a, uint32_t blocks, hipStream_t stream) {
+    HistArgs copy = a;
+    void* args[] = {&copy};
+    const size_t lds = (size_t)(a.bins + 16) * sizeof(unsigned long long);
+    return hipLaunchKernel((const void*)ssa_hist, dim3(blocks), dim3(kHistBlock), args, lds, stream);
+}
+
+}  // namespace ecdna

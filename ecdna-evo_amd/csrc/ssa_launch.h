@@ -1,0 +1,61 @@
+// ssa_launch.h — host-visible kernel argument blocks and launch wrappers shared by
+// ssa_kernels.hip (device code) and ssa_api.cpp (the C ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ecdna_ssa.h"
+
+namespace ecdna {
+
+// One chunk of replicates for the persistent SSA stepper.
+struct StepperArgs {
+    uint16_t* rows;                 // [n][row_stride] per-replicate N+ rows (replicate-major)
+    ecdna_rep_summary_t* summaries; // [n], already offset to the chunk
+    uint32_t* head;                 // work counter (zeroed before the launch)
+    const float4* rates;            // [n_param_sets] (b0, b1, d0, d1)
+    const uint16_t* init_copies;
+    const uint32_t* init_offsets;   // [n_sets + 1] or nullptr (shared initial distribution)
+    const uint64_t* init_nminus_set;// [n_sets] or nullptr
+    uint64_t row_stride;            // cells per row (multiple of 64 -> 128-B aligned rows)
+    uint64_t seed;
+    uint64_t rid0;                  // global id of the chunk's first replicate
+    uint64_t reps_per_set;
+    uint64_t max_cells;
+    uint64_t init_nminus;
+    double max_time;
+    float max_time32;
+    uint32_t n;                     // replicates in the chunk
+    uint32_t init_nplus;
+    uint32_t max_iter;
+    uint32_t cell_cap;
+    uint32_t flags;
+    uint32_t cells_mul;             // 2 under ECDNA_FLAG_BD_CAP_COMPAT for birth-death, else 1
+};
+
+// Histogram / totals pass over one chunk.
+struct HistArgs {
+    const uint16_t* rows;
+    const ecdna_rep_summary_t* summaries; // chunk-offset
+    uint64_t* hist;                       // [n_sets][bins]
+    unsigned long long* totals;           // [n_sets][16] (ecdna_totals_t as u64 words)
+    uint64_t row_stride;
+    uint64_t rid0;
+    uint64_t reps_per_set;
+    uint32_t n;
+    uint32_t bins;
+    uint32_t reps_per_block;
+};
+
+constexpr int kStepperBlock = 256;
+constexpr int kHistBlock = 256;
+constexpr uint32_t kMaxHistBins = 4096;  // LDS: 8 B per bin per workgroup (<= 64 KiB)
+
+// Kernel handle for occupancy queries and the launch itself.
+const void* stepper_kernel(int birth_death, int segregation);
+hipError_t launch_stepper(const StepperArgs& a, int birth_death, int segregation, uint32_t blocks,
+                          hipStream_t stream);
+hipError_t launch_hist(const HistArgs& a, uint32_t blocks, hipStream_t stream);
+
+}  // namespace ecdna

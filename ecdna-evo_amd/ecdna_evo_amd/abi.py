@@ -1,0 +1,228 @@
+"""ctypes mirror of include/ecdna_ssa.h (the engine's C ABI).
+
+Structs, enums and a `RunSpec` builder that turns the reference's run options
+(`SimulationOptions`, src/main.rs:27-44, built by `Cli::build`,
+src/clap_app.rs:137-229) into an `ecdna_ssa_params_t` whose host arrays stay
+alive as long as the RunSpec does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+ABI_VERSION = 1
+
+# ecdna_process_t (ProcessType, src/clap_app.rs:311-315)
+PURE_BIRTH = 0
+BIRTH_DEATH = 1
+
+# ecdna_seg_t (SegregationOptions, src/clap_app.rs:232-238)
+SEG_DETERMINISTIC = 0
+SEG_BINOMIAL = 1
+SEG_BINOMIAL_NO_UNEVEN = 2
+SEG_BINOMIAL_NO_NMINUS = 3
+SEGREGATION_NAMES = {
+    "deterministic": SEG_DETERMINISTIC,
+    "binomial": SEG_BINOMIAL,
+    "binomial-no-uneven": SEG_BINOMIAL_NO_UNEVEN,
+    "binomial-no-nminus": SEG_BINOMIAL_NO_NMINUS,
+}
+
+# ecdna_event_t (channel order, src/main.rs:140-145)
+EV_PROLIF_NMINUS, EV_PROLIF_NPLUS, EV_DEATH_NMINUS, EV_DEATH_NPLUS = 0, 1, 2, 3
+
+# ecdna_stop_t
+STOP_NONE, STOP_MAX_CELLS, STOP_MAX_TIME, STOP_MAX_ITER, STOP_ABSORBING, STOP_ERROR = range(6)
+STOP_NAMES = ["None", "MaxCells", "MaxTime", "MaxIter", "Absorbing", "Error"]
+
+# ecdna_rep_error_t
+REP_OK, REP_ERR_OVERFLOW, REP_ERR_EMPTY, REP_ERR_CELL_CAP, REP_ERR_REJECTION = range(5)
+
+FLAG_TIME_F32 = 0x1
+FLAG_BD_CAP_COMPAT = 0x2
+FLAG_EVENT_HASH = 0x4
+
+OK = 0
+E_INVALID, E_HIP, E_NOMEM, E_NODEVICE, E_STATE = -1, -2, -3, -4, -5
+
+MAX_ITER = 1_000_000_000  # src/main.rs:23
+MAX_CELLS = 1_000_000_000  # src/main.rs:25
+
+
+class Rates(C.Structure):
+    _fields_ = [("b0", C.c_float), ("b1", C.c_float), ("d0", C.c_float), ("d1", C.c_float)]
+
+
+class Params(C.Structure):
+    _fields_ = [
+        ("process", C.c_int32),
+        ("segregation", C.c_int32),
+        ("rates", C.POINTER(Rates)),
+        ("n_param_sets", C.c_uint32),
+        ("hist_bins", C.c_uint32),
+        ("reps_per_set", C.c_uint64),
+        ("seed", C.c_uint64),
+        ("first_replicate", C.c_uint64),
+        ("n_replicates", C.c_uint64),
+        ("max_cells", C.c_uint64),
+        ("max_time", C.c_double),
+        ("max_iter", C.c_uint64),
+        ("cell_cap", C.c_uint32),
+        ("flags", C.c_uint32),
+        ("init_copies", C.POINTER(C.c_uint16)),
+        ("init_nplus", C.c_uint32),
+        ("reserved0", C.c_uint32),
+        ("init_nminus", C.c_uint64),
+        ("init_set_offsets", C.POINTER(C.c_uint32)),
+        ("init_set_nminus", C.POINTER(C.c_uint64)),
+        ("device", C.c_int32),
+        ("reserved1", C.c_int32),
+    ]
+
+
+SUMMARY_DTYPE = np.dtype(
+    [
+        ("nminus", "<u8"),
+        ("nplus", "<u8"),
+        ("iters", "<u8"),
+        ("events_by_type", "<u8", (4,)),
+        ("uneven", "<u8"),
+        ("time", "<f8"),
+        ("event_hash", "<u8"),
+        ("stop_reason", "<u4"),
+        ("error", "<u4"),
+    ]
+)
+assert SUMMARY_DTYPE.itemsize == 88
+
+TOTALS_DTYPE = np.dtype(
+    [
+        ("replicates", "<u8"),
+        ("events", "<u8"),
+        ("events_by_type", "<u8", (4,)),
+        ("uneven", "<u8"),
+        ("nminus", "<u8"),
+        ("nplus", "<u8"),
+        ("stop_reasons", "<u8", (6,)),
+        ("errors", "<u8"),
+    ]
+)
+assert TOTALS_DTYPE.itemsize == 128
+
+
+def _ptr(arr: Optional[np.ndarray], ctype):
+    if arr is None:
+        return C.POINTER(ctype)()
+    return arr.ctypes.data_as(C.POINTER(ctype))
+
+
+@dataclass
+class RunSpec:
+    """One run of `n_replicates` replicates — the batched form of run_simulations (src/main.rs:55-211)."""
+
+    process: int = PURE_BIRTH
+    segregation: int = SEG_BINOMIAL
+    rates: Sequence[Sequence[float]] = ((1.0, 1.0, 0.0, 0.0),)  # [b0, b1, d0, d1] per set
+    reps_per_set: Optional[int] = None  # default: all replicates in set 0
+    seed: int = 26  # src/clap_app.rs:63
+    first_replicate: int = 0
+    n_replicates: int = 12  # src/clap_app.rs:89
+    max_cells: int = 1000  # src/clap_app.rs:149
+    max_time: Optional[float] = None  # default: floor(log2(cells) + 4), src/clap_app.rs:151
+    max_iter: int = MAX_ITER
+    cell_cap: Optional[int] = None  # default: max(max_cells, largest initial N+ count)
+    hist_bins: int = 1025
+    flags: int = FLAG_EVENT_HASH
+    init: Optional[Dict[int, int]] = None  # histogram {copies: cells}; default {1: 1} (src/clap_app.rs:188-191)
+    init_per_set: Optional[List[Dict[int, int]]] = None
+    device: int = 0
+    _keep: list = field(default_factory=list, repr=False)
+
+    def resolved_max_time(self) -> float:
+        if self.max_time is not None:
+            return float(self.max_time)
+        # (f32::log2(cells as f32) + 4f32) as u64, then `years as f32`
+        years = np.log2(np.float32(self.max_cells)) + np.float32(4.0)
+        return float(np.float32(int(years)))
+
+    @staticmethod
+    def _copies_of(hist: Dict[int, int]):
+        """EcDNADistribution::new from a histogram: n- = hist[0], one u16 per N+ cell, keys sorted
+        (the reference iterates a HashMap, whose order is random per process: SURVEY.md App. A.2)."""
+        nminus = int(hist.get(0, 0))
+        cells = []
+        for k in sorted(int(k) for k in hist if int(k) > 0):
+            if k > 65535:
+                raise ValueError(f"copy number {k} does not fit u16")
+            cells.extend([k] * int(hist[k]))
+        return np.asarray(cells, dtype=np.uint16), nminus
+
+    def params(self) -> Params:
+        self._keep = []
+        rates = np.asarray(self.rates, dtype=np.float32).reshape(-1, 4)
+        n_sets = rates.shape[0]
+        rates_arr = (Rates * n_sets)(*[Rates(*map(float, r)) for r in rates])
+        self._keep.append(rates_arr)
+        p = Params()
+        p.process = self.process
+        p.segregation = self.segregation
+        p.rates = C.cast(rates_arr, C.POINTER(Rates))
+        p.n_param_sets = n_sets
+        p.hist_bins = self.hist_bins
+        rps = self.reps_per_set
+        if rps is None:
+            rps = max(1, self.first_replicate + self.n_replicates)
+        p.reps_per_set = rps
+        p.seed = self.seed
+        p.first_replicate = self.first_replicate
+        p.n_replicates = self.n_replicates
+        p.max_cells = self.max_cells
+        p.max_time = self.resolved_max_time()
+        p.max_iter = self.max_iter
+        p.flags = self.flags
+        p.device = self.device
+        max_np = 0
+        if self.init_per_set is not None:
+            if len(self.init_per_set) != n_sets:
+                raise ValueError("init_per_set needs one histogram per parameter set")
+            parts = [self._copies_of(h) for h in self.init_per_set]
+            offs = np.zeros(n_sets + 1, dtype=np.uint32)
+            offs[1:] = np.cumsum([len(c) for c, _ in parts])
+            copies = np.concatenate([c for c, _ in parts]).astype(np.uint16) if offs[-1] else np.zeros(1, np.uint16)
+            nms = np.asarray([nm for _, nm in parts], dtype=np.uint64)
+            self._keep += [copies, offs, nms]
+            p.init_copies = _ptr(copies, C.c_uint16)
+            p.init_nplus = 0
+            p.init_nminus = 0
+            p.init_set_offsets = _ptr(offs, C.c_uint32)
+            p.init_set_nminus = _ptr(nms, C.c_uint64)
+            max_np = int(np.max(np.diff(offs))) if n_sets else 0
+        else:
+            copies, nm = self._copies_of(self.init if self.init is not None else {1: 1})
+            buf = copies if len(copies) else np.zeros(1, np.uint16)
+            self._keep.append(buf)
+            p.init_copies = _ptr(buf, C.c_uint16)
+            p.init_nplus = len(copies)
+            p.init_nminus = nm
+            max_np = len(copies)
+        cap = self.cell_cap
+        if cap is None:
+            cap = max(int(min(self.max_cells, 2**32 - 1)), max_np, 1)
+        p.cell_cap = cap
+        return p
+
+
+def summaries_array(n: int) -> np.ndarray:
+    return np.zeros(n, dtype=SUMMARY_DTYPE)
+
+
+def totals_array(n_sets: int) -> np.ndarray:
+    return np.zeros(n_sets, dtype=TOTALS_DTYPE)
+
+
+def as_ptr(arr: np.ndarray):
+    return C.c_void_p(arr.ctypes.data)

@@ -1,0 +1,218 @@
+/*
+ * ecdna_ssa.h — C ABI of the MI355X many-replicate Gillespie SSA engine for
+ * ecDNA birth–death–segregation dynamics.
+ *
+ * This is the drop-in boundary for the reference's hot path. In
+ * fraterenz/ecdna-evo v0.26.0 every replicate is one call of
+ *
+ *     sosa::simulate(&mut state, &rates, &reactions, &mut process, &options, &mut rng)
+ *
+ * (src/main.rs:92-99 for PureBirth, src/main.rs:166-173 for BirthDeath), made
+ * once per replicate index idx by the closure run_simulations
+ * (src/main.rs:55-211) that rayon maps over seed*10 .. seed*10+runs
+ * (src/main.rs:212-225). Inside that call run the process model
+ * (AdvanceStep::advance_step / update_state, src/process.rs:114-197 and
+ * src/process.rs:259-345), the event kernels (Exponential::increase_nplus,
+ * increase_nminus, CellDeath::decrease_nplus / decrease_nminus,
+ * src/proliferation.rs:24-140) and the segregation rules
+ * (src/segregation.rs:110-194).
+ *
+ * Here ONE call runs ALL replicates of a run on one GPU (one replicate per
+ * GPU lane): ecdna_ssa_run() replaces the R calls of simulate() that the
+ * rayon loop makes, and returns what run_simulations keeps of each one
+ * (stop reason, final [n-, n+] and time: src/main.rs:124-128, 198-210) plus
+ * the pooled copy-number histogram that process::save writes per replicate
+ * (src/process.rs:31-55; JSON body {"0": n-, "k": cells}, dynamics.md:8).
+ *
+ * Conventions: plain C types only; no exceptions cross the boundary; every
+ * buffer is caller-owned; functions return 0 on success or a negative
+ * ECDNA_E_* code (ecdna_ssa_strerror). Per-replicate failures that the
+ * reference turns into panics are reported in ecdna_rep_summary_t.error.
+ *
+ * RNG: replicate r (a GLOBAL id, so shards on different GPUs draw the same
+ * streams as one big run) uses Philox4x32-10 with key = (seed lo, seed hi)
+ * and counter = (event index, sub-block, r lo, r hi). The draw mapping is
+ * spelled out in DESIGN.md §3; oracle/ restates it on the CPU bit for bit.
+ */
+#ifndef ECDNA_SSA_H
+#define ECDNA_SSA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ECDNA_SSA_ABI_VERSION 1
+
+/* Process type — ProcessType (src/clap_app.rs:311-315); chosen as BirthDeath
+ * when d0 > 0 or d1 > 0 (src/clap_app.rs:163-174, 194-200). */
+typedef enum {
+    ECDNA_PURE_BIRTH = 0,  /* channels [ProliferateNMinus, ProliferateNPlus]  src/main.rs:67-71 */
+    ECDNA_BIRTH_DEATH = 1  /* + [DeathNMinus, DeathNPlus]                     src/main.rs:139-145 */
+} ecdna_process_t;
+
+/* Segregation rule — SegregationOptions (src/clap_app.rs:232-238). */
+typedef enum {
+    ECDNA_SEG_DETERMINISTIC = 0,      /* Deterministic      src/segregation.rs:142-155 */
+    ECDNA_SEG_BINOMIAL = 1,           /* Binomial           src/segregation.rs:110-140 */
+    ECDNA_SEG_BINOMIAL_NO_UNEVEN = 2, /* BinomialNoUneven   src/segregation.rs:157-174 */
+    ECDNA_SEG_BINOMIAL_NO_NMINUS = 3  /* BinomialNoNminus   src/segregation.rs:176-194 */
+} ecdna_seg_t;
+
+/* Reaction channels, in the reference's channel order (src/main.rs:140-145).
+ * EcDNAEvent (src/process.rs:20-29) declares 7 variants; only these 4 are
+ * reachable (src/process.rs:179, 331). */
+typedef enum {
+    ECDNA_EV_PROLIF_NMINUS = 0,
+    ECDNA_EV_PROLIF_NPLUS = 1,
+    ECDNA_EV_DEATH_NMINUS = 2,
+    ECDNA_EV_DEATH_NPLUS = 3
+} ecdna_event_t;
+
+/* Why a replicate stopped (sosa::StopReason; checked in this order before
+ * every event). */
+typedef enum {
+    ECDNA_STOP_NONE = 0,       /* never started (see error) */
+    ECDNA_STOP_MAX_CELLS = 1,  /* n- + n+ >= max_cells        (Options.max_cells, src/clap_app.rs:207) */
+    ECDNA_STOP_MAX_TIME = 2,   /* t >= max_time               (IterTime.time, src/clap_app.rs:205) */
+    ECDNA_STOP_MAX_ITER = 3,   /* iterations >= max_iter      (MAX_ITER, src/main.rs:23) */
+    ECDNA_STOP_ABSORBING = 4,  /* total propensity == 0 (extinction) */
+    ECDNA_STOP_ERROR = 5       /* see ecdna_rep_summary_t.error */
+} ecdna_stop_t;
+
+/* Per-replicate errors — where the reference panics or refuses. */
+typedef enum {
+    ECDNA_REP_OK = 0,
+    ECDNA_REP_ERR_OVERFLOW = 1,   /* 2k > u16::MAX: checked_mul panic, src/proliferation.rs:63-67 */
+    ECDNA_REP_ERR_EMPTY = 2,      /* empty initial distribution: ensure!, src/process.rs:88, 232 */
+    ECDNA_REP_ERR_CELL_CAP = 3,   /* N+ row would exceed cell_cap (the reference grows a Vec) */
+    ECDNA_REP_ERR_REJECTION = 4   /* BinomialNoUneven loop exceeded 4096 redraws (p < 2^-4096) */
+} ecdna_rep_error_t;
+
+/* Flags (ecdna_ssa_params_t.flags). */
+#define ECDNA_FLAG_TIME_F32 0x1u       /* accumulate time in f32 like process.time (src/process.rs:68, 184) */
+#define ECDNA_FLAG_BD_CAP_COMPAT 0x2u  /* BD: stop at 2(n- + n+) >= max_cells, i.e. sum of the
+                                          duplicated population vector (src/process.rs:339-344) */
+#define ECDNA_FLAG_EVENT_HASH 0x4u     /* fold every event into ecdna_rep_summary_t.event_hash */
+
+/* API return codes. */
+#define ECDNA_OK 0
+#define ECDNA_E_INVALID (-1)   /* bad parameter */
+#define ECDNA_E_HIP (-2)       /* HIP runtime error */
+#define ECDNA_E_NOMEM (-3)     /* device allocation failed */
+#define ECDNA_E_NODEVICE (-4)  /* no usable gfx950 device */
+#define ECDNA_E_STATE (-5)     /* call order (e.g. download before launch) */
+
+/* Rates of one parameter set: ReactionRates([b0, b1, d0, d1]) (src/main.rs:67, 139). f32 as in Cli
+ * (src/clap_app.rs:41-55). */
+typedef struct {
+    float b0, b1, d0, d1;
+} ecdna_rates_t;
+
+/* One run = n_replicates independent replicates with global ids
+ * first_replicate .. first_replicate + n_replicates - 1.
+ * Replicate r uses parameter set s = r / reps_per_set (must be < n_param_sets). */
+typedef struct {
+    int32_t process;                /* ecdna_process_t */
+    int32_t segregation;            /* ecdna_seg_t */
+    const ecdna_rates_t* rates;     /* host, [n_param_sets] */
+    uint32_t n_param_sets;          /* 1, or e.g. 1024 for an ABC sweep */
+    uint32_t hist_bins;             /* bins per set: bin 0 = N- cells, bin k = cells with k copies,
+                                       bin hist_bins-1 = cells with >= hist_bins-1 copies; >= 2 */
+    uint64_t reps_per_set;          /* replicates per parameter set (>= 1) */
+    uint64_t seed;                  /* --seed (src/clap_app.rs:63) */
+    uint64_t first_replicate;       /* global id of the first replicate of this call (sharding) */
+    uint64_t n_replicates;          /* replicates in this call */
+    uint64_t max_cells;             /* stop when n- + n+ >= max_cells (src/clap_app.rs:142-157) */
+    double max_time;                /* stop when t >= max_time (years; src/clap_app.rs:151, 205) */
+    uint64_t max_iter;              /* stop after max_iter events (1e9, src/main.rs:23); < 2^32 */
+    uint32_t cell_cap;              /* capacity of the per-replicate N+ row (cells); rounded up to 64 */
+    uint32_t flags;                 /* ECDNA_FLAG_* */
+    /* Initial distribution (EcDNADistribution: n- plus one u16 per N+ cell; default {1: 1},
+     * src/clap_app.rs:188-191). Either shared by every set (init_set_offsets == NULL: copies
+     * init_copies[0 .. init_nplus), n- = init_nminus) or per set (init_set_offsets[n_param_sets+1]
+     * into init_copies, init_set_nminus[n_param_sets]). Copy numbers must be >= 1. */
+    const uint16_t* init_copies;    /* host */
+    uint32_t init_nplus;
+    uint32_t reserved0;
+    uint64_t init_nminus;
+    const uint32_t* init_set_offsets; /* host or NULL */
+    const uint64_t* init_set_nminus;  /* host or NULL */
+    int32_t device;                 /* HIP device ordinal for ecdna_ssa_run / ctx_create */
+    int32_t reserved1;
+} ecdna_ssa_params_t;
+
+/* What run_simulations keeps of one replicate (src/main.rs:124-128, 198-210), plus counters. */
+typedef struct {
+    uint64_t nminus;                /* final n-  (population[0]) */
+    uint64_t nplus;                 /* final n+  (population[1]) */
+    uint64_t iters;                 /* events executed = advance_step calls */
+    uint64_t events_by_type[4];     /* per ecdna_event_t */
+    uint64_t uneven;                /* ProliferateNPlus events with a complete uneven split */
+    double time;                    /* final process.time (years) */
+    uint64_t event_hash;            /* FNV-1a fold of (event, k1, cell index) per event, if enabled */
+    uint32_t stop_reason;           /* ecdna_stop_t */
+    uint32_t error;                 /* ecdna_rep_error_t */
+} ecdna_rep_summary_t;
+
+/* Per-parameter-set sums over the replicates of a call. */
+typedef struct {
+    uint64_t replicates;
+    uint64_t events;                /* sum of iters — the numerator of events/s */
+    uint64_t events_by_type[4];
+    uint64_t uneven;
+    uint64_t nminus;                /* sum of final n- */
+    uint64_t nplus;                 /* sum of final n+ */
+    uint64_t stop_reasons[6];       /* per ecdna_stop_t */
+    uint64_t errors;                /* replicates with error != 0 */
+} ecdna_totals_t;
+
+int ecdna_ssa_abi_version(void);
+const char* ecdna_ssa_strerror(int code);
+/* Detail of the last failure on the calling thread ("" if none). */
+const char* ecdna_ssa_last_error_message(void);
+
+/* Number of usable gfx950 devices (0 when none). */
+int ecdna_ssa_device_count(void);
+
+/* One-shot: runs every replicate of *p on device p->device and copies the results to HOST buffers
+ * (each may be NULL): out_summaries[n_replicates] (replicate first_replicate + i at index i),
+ * out_hist[n_param_sets * hist_bins] (zeroed, then filled), out_totals[n_param_sets].
+ * stream: a hipStream_t, or NULL for a private stream. Blocks until done. */
+int ecdna_ssa_run(const ecdna_ssa_params_t* p, ecdna_rep_summary_t* out_summaries,
+                  uint64_t* out_hist, ecdna_totals_t* out_totals, void* stream);
+
+/* Device-resident context for repeated runs (benchmarks, multi-GPU). Inputs are uploaded once at
+ * create; rows/summaries/histogram stay in HBM between launches. */
+typedef struct ecdna_ssa_ctx ecdna_ssa_ctx;
+
+int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out);
+/* Use caller-owned DEVICE buffers for the histogram [n_param_sets*hist_bins] u64 and totals
+ * [n_param_sets] (e.g. tensors later all-reduced over RCCL). NULL keeps the internal buffer. */
+int ecdna_ssa_ctx_set_outputs(ecdna_ssa_ctx* c, uint64_t* d_hist, ecdna_totals_t* d_totals);
+/* Enqueue one full run on `stream` (NULL = the context's stream): zero hist/totals, SSA kernel over
+ * all replicates (in memory-bounded chunks), histogram kernel. Asynchronous. */
+int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream);
+/* Block until the last launch finished; returns its device time in ms (HIP events on the launch
+ * stream): ssa_ms = SSA stepper kernels only, hist_ms = histogram/summary kernels. Either may be NULL. */
+int ecdna_ssa_ctx_sync(ecdna_ssa_ctx* c, float* ssa_ms, float* hist_ms);
+/* Device pointers of the current outputs. */
+int ecdna_ssa_ctx_device_outputs(ecdna_ssa_ctx* c, uint64_t** d_hist, ecdna_totals_t** d_totals);
+/* Copy results of the last launch to HOST buffers (each may be NULL). out_rows, if given, receives
+ * [n_replicates][row_stride] u16 where row i holds the final N+ copies of replicate i in the
+ * engine's swap_remove order (entries past summaries[i].nplus are unspecified). Valid only when the
+ * whole run fit in one chunk (ecdna_ssa_ctx_row_stride returns > 0). */
+int ecdna_ssa_ctx_download(ecdna_ssa_ctx* c, ecdna_rep_summary_t* out_summaries, uint64_t* out_hist,
+                           ecdna_totals_t* out_totals, uint16_t* out_rows);
+/* Row stride (cells) of the rows buffer, or 0 when the run is chunked (rows not downloadable). */
+int64_t ecdna_ssa_ctx_row_stride(const ecdna_ssa_ctx* c);
+/* Replicates per chunk (memory bound) and lanes of the persistent stepper grid. */
+int ecdna_ssa_ctx_geometry(const ecdna_ssa_ctx* c, uint64_t* chunk_replicates, uint64_t* grid_lanes);
+int ecdna_ssa_ctx_destroy(ecdna_ssa_ctx* c);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ECDNA_SSA_H */

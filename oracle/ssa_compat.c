@@ -1,0 +1,476 @@
+/*
+ * ssa_compat.c — TEST INFRASTRUCTURE ONLY (see ssa_oracle.h). The
+ * reference-semantics CPU path ("chacha8-compat"): the same event loop as
+ * ssa_oracle.c but with the reference's RNG stack and samplers, as pinned in
+ * Cargo.lock and reconstructed from their published algorithms (the crates
+ * are not vendored, no Rust toolchain exists here, so seed-for-seed equality
+ * with the Rust binary is unverified — "parity unpinned"; it is matched in
+ * distribution):
+ *
+ *   rand_chacha 0.3.1 ChaCha8Rng (Cargo.lock:813-821): ChaCha, 8 rounds,
+ *     64-bit block counter in words 12-13, stream in words 14-15, a 4-block
+ *     (64-word) output buffer; seed_from_u64 = rand_core 0.6.4 PCG32 key
+ *     expansion (Cargo.lock:823-829). Stream = seed*10 + i (src/main.rs:56-58,
+ *     213-215).
+ *   rand 0.8.5 (Cargo.lock:802-810): gen_range(0..n) over usize =
+ *     widening-multiply rejection on next_u64; gen::<f64>() = 53 high bits.
+ *   rand_distr 0.4.3 (Cargo.lock:832-839): Exp1 by the 256-layer ziggurat
+ *     (Marsaglia & Tsang 2000) with Exp::sample = Exp1 as f32 * (1/lambda);
+ *     Binomial by BINV inversion for n*p < 10, else BTPE
+ *     (Kachitvichyanukul & Schmeiser 1988, GSL sign convention).
+ *   sosa 3.0.3 (Cargo.lock:944-955): first-reaction method, tau_i ~ Exp(rate_i
+ *     * pop_i) per channel in channel order, no draw for a zero propensity,
+ *     argmin (first on ties); process.time accumulated in f32
+ *     (src/process.rs:184, 336).
+ *   ecdna-lib 3.0.2: pick_remove_random_nplus/decrease_nplus = gen_range +
+ *     swap_remove; increase_nplus = push.
+ *
+ * Event semantics (src/process.rs:147-184, 291-336; src/proliferation.rs:25-140;
+ * src/segregation.rs:110-194) are shared with ssa_oracle.c.
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "ssa_oracle.h"
+
+/* ------------------------------------------------------------ ChaCha8Rng */
+
+#define ROTL(x, n) (((x) << (n)) | ((x) >> (32 - (n))))
+#define QR(a, b, c, d)          \
+    a += b;                     \
+    d ^= a;                     \
+    d = ROTL(d, 16);            \
+    c += d;                     \
+    b ^= c;                     \
+    b = ROTL(b, 12);            \
+    a += b;                     \
+    d ^= a;                     \
+    d = ROTL(d, 8);             \
+    c += d;                     \
+    b ^= c;                     \
+    b = ROTL(b, 7);
+
+void oracle_chacha_block(const uint32_t in[16], uint32_t out[16], int rounds) {
+    uint32_t x[16];
+    memcpy(x, in, sizeof(x));
+    for (int i = 0; i < rounds; i += 2) {
+        QR(x[0], x[4], x[8], x[12]);
+        QR(x[1], x[5], x[9], x[13]);
+        QR(x[2], x[6], x[10], x[14]);
+        QR(x[3], x[7], x[11], x[15]);
+        QR(x[0], x[5], x[10], x[15]);
+        QR(x[1], x[6], x[11], x[12]);
+        QR(x[2], x[7], x[8], x[13]);
+        QR(x[3], x[4], x[9], x[14]);
+    }
+    for (int i = 0; i < 16; ++i) out[i] = x[i] + in[i];
+}
+
+void oracle_chacha_seed_from_u64(uint64_t state, uint32_t key[8]) {
+    const uint64_t MUL = 6364136223846793005ull, INC = 11634580027462260723ull;
+    for (int i = 0; i < 8; ++i) {
+        state = state * MUL + INC;
+        uint32_t xorshifted = (uint32_t)(((state >> 18) ^ state) >> 27);
+        uint32_t rot = (uint32_t)(state >> 59);
+        key[i] = (xorshifted >> rot) | (xorshifted << ((32 - rot) & 31));
+    }
+}
+
+struct oracle_chacha {
+    uint32_t st[16];
+    uint32_t buf[64];
+    uint32_t idx;
+};
+
+static void chacha_init(oracle_chacha* r, uint64_t seed, uint64_t stream) {
+    r->st[0] = 0x61707865u;
+    r->st[1] = 0x3320646eu;
+    r->st[2] = 0x79622d32u;
+    r->st[3] = 0x6b206574u;
+    oracle_chacha_seed_from_u64(seed, &r->st[4]);
+    r->st[12] = 0;
+    r->st[13] = 0;
+    r->st[14] = (uint32_t)stream;
+    r->st[15] = (uint32_t)(stream >> 32);
+    r->idx = 64;
+}
+
+static void chacha_refill(oracle_chacha* r) {
+    for (int b = 0; b < 4; ++b) {
+        oracle_chacha_block(r->st, &r->buf[16 * b], 8);
+        uint64_t c = ((uint64_t)r->st[13] << 32 | r->st[12]) + 1;
+        r->st[12] = (uint32_t)c;
+        r->st[13] = (uint32_t)(c >> 32);
+    }
+}
+
+static inline uint32_t cc_u32(oracle_chacha* r) {
+    if (r->idx >= 64) {
+        chacha_refill(r);
+        r->idx = 0;
+    }
+    return r->buf[r->idx++];
+}
+
+/* rand_core BlockRng::next_u64: two consecutive words, low first, spanning a refill. */
+static inline uint64_t cc_u64(oracle_chacha* r) {
+    if (r->idx < 63) {
+        uint64_t lo = r->buf[r->idx], hi = r->buf[r->idx + 1];
+        r->idx += 2;
+        return hi << 32 | lo;
+    }
+    if (r->idx >= 64) {
+        chacha_refill(r);
+        r->idx = 2;
+        return (uint64_t)r->buf[1] << 32 | r->buf[0];
+    }
+    uint64_t lo = r->buf[63];
+    chacha_refill(r);
+    r->idx = 1;
+    return (uint64_t)r->buf[0] << 32 | lo;
+}
+
+oracle_chacha* oracle_chacha_new(uint64_t seed, uint64_t stream) {
+    oracle_chacha* r = malloc(sizeof(*r));
+    chacha_init(r, seed, stream);
+    return r;
+}
+void oracle_chacha_free(oracle_chacha* r) { free(r); }
+uint32_t oracle_chacha_next_u32(oracle_chacha* r) { return cc_u32(r); }
+uint64_t oracle_chacha_next_u64(oracle_chacha* r) { return cc_u64(r); }
+
+/* ---------------------------------------------------------- rand samplers */
+
+/* gen_range(0..n), usize: UniformInt::sample_single (rand 0.8.5). */
+static uint64_t gen_range(oracle_chacha* r, uint64_t n) {
+    uint64_t zone = (n << __builtin_clzll(n)) - 1;
+    for (;;) {
+        uint64_t v = cc_u64(r);
+        unsigned __int128 m = (unsigned __int128)v * n;
+        uint64_t lo = (uint64_t)m;
+        if (lo <= zone) return (uint64_t)(m >> 64);
+    }
+}
+uint64_t oracle_compat_gen_range(oracle_chacha* r, uint64_t n) { return gen_range(r, n); }
+
+/* Standard f64: (next_u64 >> 11) * 2^-53. */
+static inline double gen_f64(oracle_chacha* r) { return (double)(cc_u64(r) >> 11) * 0x1p-53; }
+
+/* bits >> 12 as the mantissa of a value in [1, 2). */
+static inline double float_1_2(uint64_t bits) {
+    union {
+        uint64_t u;
+        double d;
+    } x;
+    x.u = 0x3FF0000000000000ull | (bits >> 12);
+    return x.d;
+}
+
+/* Exp1 ziggurat tables: 256 layers, R = 7.69711747013104972, V = (R+1) e^-R. */
+#define ZIG_EXP_R 7.697117470131487
+static double zig_x[257], zig_f[257];
+static int zig_ready = 0;
+
+static void zig_init(void) {
+    if (zig_ready) return;
+    const double R = ZIG_EXP_R;
+    const double V = (R + 1.0) * exp(-R);
+    zig_x[0] = V / exp(-R);
+    zig_x[1] = R;
+    for (int i = 1; i < 256; ++i) zig_x[i + 1] = -log(exp(-zig_x[i]) + V / zig_x[i]);
+    zig_x[256] = 0.0;
+    for (int i = 0; i < 257; ++i) zig_f[i] = exp(-zig_x[i]);
+    zig_f[256] = 1.0;
+    __atomic_store_n(&zig_ready, 1, __ATOMIC_RELEASE);
+}
+
+static double exp1(oracle_chacha* r) {
+    for (;;) {
+        uint64_t bits = cc_u64(r);
+        int i = (int)(bits & 0xff);
+        double u = float_1_2(bits) - (1.0 - 0x1p-53);
+        double x = u * zig_x[i];
+        if (x < zig_x[i + 1]) return x;
+        if (i == 0) return ZIG_EXP_R - log(gen_f64(r));
+        if (zig_f[i + 1] + (zig_f[i] - zig_f[i + 1]) * gen_f64(r) < exp(-x)) return x;
+    }
+}
+double oracle_compat_exp1(oracle_chacha* r) {
+    zig_init();
+    return exp1(r);
+}
+
+static inline int64_t f64_to_i64(double x) { return (int64_t)x; }
+
+static double stirling(double a) {
+    double a2 = a * a;
+    return (13860. - (462. - (132. - (99. - 140. / a2) / a2) / a2) / a2) / a / 166320.;
+}
+
+/* rand_distr 0.4.3 Binomial::sample. */
+static uint64_t binomial(oracle_chacha* rg, uint64_t n_u, double p_in) {
+    if (p_in == 0.0) return 0;
+    if (p_in == 1.0) return n_u;
+    double p = p_in <= 0.5 ? p_in : 1.0 - p_in;
+    double q = 1.0 - p;
+    uint64_t result;
+    if ((double)n_u * p < 10.0 && n_u <= 0x7fffffffull) {
+        /* BINV */
+        double s = p / q;
+        double a = (double)(n_u + 1) * s;
+        for (;;) {
+            double r = pow(q, (double)n_u);
+            double u = gen_f64(rg);
+            uint64_t x = 0;
+            int restart = 0;
+            while (u > r) {
+                u -= r;
+                x += 1;
+                if (x > 110) {
+                    restart = 1;
+                    break;
+                }
+                r *= a / (double)x - s;
+            }
+            if (!restart) {
+                result = x;
+                break;
+            }
+        }
+    } else {
+        /* BTPE */
+        const int64_t SQUEEZE = 20;
+        double n = (double)n_u;
+        double np = n * p;
+        double npq = np * q;
+        double f_m = np + p;
+        int64_t m = f64_to_i64(f_m);
+        double p1 = floor(2.195 * sqrt(npq) - 4.6 * q) + 0.5;
+        double x_m = (double)m + 0.5;
+        double x_l = x_m - p1;
+        double x_r = x_m + p1;
+        double c = 0.134 + 20.5 / (15.3 + (double)m);
+        double p2 = p1 * (1. + 2. * c);
+        double al = (f_m - x_l) / (f_m - x_l * p);
+        double lambda_l = al * (1. + 0.5 * al);
+        double ar = (x_r - f_m) / (x_r * q);
+        double lambda_r = ar * (1. + 0.5 * ar);
+        double p3 = p2 + c / lambda_l;
+        double p4 = p3 + c / lambda_r;
+        int64_t y;
+        for (;;) {
+            double u = (float_1_2(cc_u64(rg)) - 1.0) * p4;
+            double v = float_1_2(cc_u64(rg)) - 1.0;
+            if (!(u > p1)) {
+                y = f64_to_i64(x_m - p1 * v + u);
+                break;
+            }
+            if (!(u > p2)) {
+                double x = x_l + (u - p1) / c;
+                v = v * c + 1.0 - fabs(x - x_m) / p1;
+                if (v > 1.) continue;
+                y = f64_to_i64(x);
+            } else if (!(u > p3)) {
+                y = f64_to_i64(x_l + log(v) / lambda_l);
+                if (y < 0) continue;
+                v *= (u - p2) * lambda_l;
+            } else {
+                y = f64_to_i64(x_r - log(v) / lambda_r);
+                if (y > 0 && (uint64_t)y > n_u) continue;
+                v *= (u - p3) * lambda_r;
+            }
+            int64_t k = llabs(y - m);
+            if (!(k > SQUEEZE && (double)k < 0.5 * npq - 1.)) {
+                double s = p / q;
+                double a = s * (n + 1.);
+                double f = 1.0;
+                if (m < y) {
+                    int64_t i = m;
+                    do {
+                        i += 1;
+                        f *= a / (double)i - s;
+                    } while (i != y);
+                } else if (m > y) {
+                    int64_t i = y;
+                    do {
+                        i += 1;
+                        f /= a / (double)i - s;
+                    } while (i != m);
+                }
+                if (v > f) continue;
+                break;
+            }
+            double kf = (double)k;
+            double rho = (kf / npq) * ((kf * (kf / 3. + 0.625) + 1. / 6.) / npq + 0.5);
+            double t = -0.5 * kf * kf / npq;
+            double alpha = log(v);
+            if (alpha < t - rho) break;
+            if (alpha > t + rho) continue;
+            double x1 = (double)(y + 1);
+            double f1 = (double)(m + 1);
+            double z = (double)(f64_to_i64(n) + 1 - m);
+            double w = (double)(f64_to_i64(n) - y + 1);
+            if (alpha > x_m * log(f1 / x1) + (n - (double)m + 0.5) * log(z / w) +
+                            (double)(y - m) * log(w * p / (x1 * q)) + stirling(f1) + stirling(z) -
+                            stirling(x1) - stirling(w))
+                continue;
+            break;
+        }
+        result = (uint64_t)y;
+    }
+    if (p != p_in) result = n_u - result;
+    return result;
+}
+uint64_t oracle_compat_binomial(oracle_chacha* r, uint64_t n, double p) { return binomial(r, n, p); }
+
+/* ------------------------------------------------------------- event loop */
+
+#define FNV_OFFSET 0xcbf29ce484222325ull
+#define FNV_PRIME 0x100000001b3ull
+
+void oracle_compat_simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16_t* row,
+                                      ecdna_rep_summary_t* out) {
+    zig_init();
+    const uint64_t set = rid / p->reps_per_set;
+    const ecdna_rates_t rt = p->rates[set];
+    const int bd = p->process == ECDNA_BIRTH_DEATH;
+    const int hash_on = (p->flags & ECDNA_FLAG_EVENT_HASH) != 0;
+    const uint64_t cells_mul = (bd && (p->flags & ECDNA_FLAG_BD_CAP_COMPAT)) ? 2u : 1u;
+    const int K = bd ? 4 : 2;
+    const float rates[4] = {rt.b0, rt.b1, rt.d0, rt.d1};
+
+    const uint16_t* init;
+    uint64_t nplus, nminus;
+    if (p->init_set_offsets) {
+        init = p->init_copies + p->init_set_offsets[set];
+        nplus = p->init_set_offsets[set + 1] - p->init_set_offsets[set];
+    } else {
+        init = p->init_copies;
+        nplus = p->init_nplus;
+    }
+    nminus = p->init_set_nminus ? p->init_set_nminus[set] : p->init_nminus;
+    memcpy(row, init, nplus * sizeof(uint16_t));
+
+    oracle_chacha rng;
+    chacha_init(&rng, p->seed, p->seed * 10u + rid); /* src/main.rs:56-58, stream = idx */
+
+    memset(out, 0, sizeof(*out));
+    uint64_t h = FNV_OFFSET;
+    float t = 0.0f;
+    const float max_t = (float)p->max_time;
+    uint64_t e = 0;
+    uint32_t stop = ECDNA_STOP_NONE, err = ECDNA_REP_OK;
+    uint64_t cnt[4] = {0, 0, 0, 0}, uneven_n = 0;
+    if (nplus == 0 && nminus == 0) {
+        err = ECDNA_REP_ERR_EMPTY;
+        stop = ECDNA_STOP_ERROR;
+    }
+    while (!stop) {
+        if (e >= p->max_iter) {
+            stop = ECDNA_STOP_MAX_ITER;
+            break;
+        }
+        if ((nminus + nplus) * cells_mul >= p->max_cells) {
+            stop = ECDNA_STOP_MAX_CELLS;
+            break;
+        }
+        if (t >= max_t) {
+            stop = ECDNA_STOP_MAX_TIME;
+            break;
+        }
+        /* first-reaction method over population [n-, n+, n-, n+] */
+        const uint64_t pop[4] = {nminus, nplus, nminus, nplus};
+        int ch = -1;
+        float best = INFINITY;
+        for (int c = 0; c < K; ++c) {
+            float lambda = rates[c] * (float)pop[c];
+            if (!(lambda > 0.0f)) continue;
+            float inv = 1.0f / lambda;
+            float tau = (float)exp1(&rng) * inv;
+            if (ch < 0 || tau < best) { /* argmin, first on ties */
+                best = tau;
+                ch = c;
+            }
+        }
+        if (ch < 0) {
+            stop = ECDNA_STOP_ABSORBING;
+            break;
+        }
+        uint64_t x = (uint64_t)ch;
+        if (ch == ECDNA_EV_PROLIF_NMINUS) {
+            nminus += 1;
+        } else if (ch == ECDNA_EV_DEATH_NMINUS) {
+            nminus -= 1;
+        } else if (ch == ECDNA_EV_DEATH_NPLUS) {
+            uint64_t i = gen_range(&rng, nplus);
+            row[i] = row[nplus - 1];
+            nplus -= 1;
+            x |= i << 20;
+        } else {
+            uint64_t i = gen_range(&rng, nplus);
+            uint32_t k = row[i];
+            if (k > 32767u) {
+                err = ECDNA_REP_ERR_OVERFLOW;
+                stop = ECDNA_STOP_ERROR;
+                break;
+            }
+            uint32_t n = 2u * k, k1 = 0;
+            int uneven = 0; /* 0 False, 1 True, 2 TrueWithoutNMinusIncrease */
+            switch (p->segregation) {
+                case ECDNA_SEG_DETERMINISTIC:
+                    k1 = n / 2;
+                    break;
+                case ECDNA_SEG_BINOMIAL:
+                    k1 = (uint32_t)binomial(&rng, n, 0.5);
+                    uneven = (k1 == 0 || k1 == n) ? 1 : 0;
+                    break;
+                case ECDNA_SEG_BINOMIAL_NO_UNEVEN: {
+                    int tries = 0;
+                    do {
+                        k1 = (uint32_t)binomial(&rng, n, 0.5);
+                    } while ((k1 == 0 || k1 == n) && ++tries < 4096);
+                    if (k1 == 0 || k1 == n) {
+                        err = ECDNA_REP_ERR_REJECTION;
+                        stop = ECDNA_STOP_ERROR;
+                    }
+                    break;
+                }
+                default:
+                    k1 = (uint32_t)binomial(&rng, n, 0.5);
+                    uneven = (k1 == 0 || k1 == n) ? 2 : 0;
+                    break;
+            }
+            if (stop) break;
+            if (uneven == 0 && nplus + 1 > p->cell_cap) {
+                err = ECDNA_REP_ERR_CELL_CAP;
+                stop = ECDNA_STOP_ERROR;
+                break;
+            }
+            row[i] = row[nplus - 1];
+            nplus -= 1;
+            if (uneven == 0) {
+                row[nplus++] = (uint16_t)k1;
+                row[nplus++] = (uint16_t)(n - k1);
+            } else {
+                if (uneven == 1) nminus += 1;
+                row[nplus++] = (uint16_t)n;
+                uneven_n += 1;
+            }
+            x |= ((uint64_t)k1 << 2) | (i << 20);
+        }
+        cnt[ch] += 1;
+        e += 1;
+        t = t + best;
+        if (hash_on) h = (h ^ x) * FNV_PRIME;
+    }
+    out->nminus = nminus;
+    out->nplus = nplus;
+    out->iters = e;
+    for (int c = 0; c < 4; ++c) out->events_by_type[c] = cnt[c];
+    out->uneven = uneven_n;
+    out->time = (double)t;
+    out->event_hash = hash_on ? h : 0;
+    out->stop_reason = stop;
+    out->error = err;
+}

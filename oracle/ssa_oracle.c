@@ -1,0 +1,570 @@
+/*
+ * ssa_oracle.c — TEST INFRASTRUCTURE ONLY (see ssa_oracle.h): plain-C
+ * restatement of the reference's per-replicate Gillespie loop, "philox" mode.
+ *
+ * It follows, function by function:
+ *   sosa::simulate loop (external crate sosa 3.0.3, Cargo.lock:944-955; call
+ *     sites src/main.rs:92-99, 166-173; Options src/clap_app.rs:202-209)
+ *     -> simulate_replicate()
+ *   PureBirth/BirthDeath::advance_step event dispatch + time accumulation
+ *     (src/process.rs:147-184, 291-336) -> the switch in simulate_replicate()
+ *   update_state population vectors (src/process.rs:187-196, 339-344)
+ *     -> propensities(): [n-, n+] / [n-, n+, n-, n+]
+ *   Exponential::increase_nplus (src/proliferation.rs:25-111) -> prolif_nplus()
+ *   Exponential::increase_nminus (src/proliferation.rs:113-117), CellDeath
+ *     (src/proliferation.rs:126-140) -> the N- cases / death_nplus()
+ *   Segregate impls (src/segregation.rs:110-194) -> segregate()
+ *   EcDNADistribution pick_remove_random_nplus / decrease_nplus =
+ *     gen_range + swap_remove, increase_nplus = push (ecdna-lib 3.0.2,
+ *     reconstructed in SURVEY.md App. A.2) -> swap_remove()/push in place
+ *   rayon over replicate ids (src/main.rs:221-224) -> pthread pool with an
+ *     atomic work counter (run_pool()).
+ *
+ * The draws follow the engine's mapping, not ChaCha8: see
+ * ssa_compat.c for the reference-semantics samplers.
+ *
+ * Floating point: compile with -ffp-contract=off. Every f64 operation below is
+ * a correctly rounded IEEE add/sub/mul/div in a fixed order, so the HIP kernel
+ * (which spells the same operations with contraction disabled) reproduces the
+ * times and channel picks bit for bit.
+ */
+#include "ssa_oracle.h"
+
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+/* ------------------------------------------------------------------ Philox */
+
+#define PHILOX_M0 0xD2511F53u
+#define PHILOX_M1 0xCD9E8D57u
+#define PHILOX_W0 0x9E3779B9u
+#define PHILOX_W1 0xBB67AE85u
+
+/* Philox4x32-10 (Salmon et al., SC'11; Random123 philox4x32 with 10 rounds). */
+void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+    uint32_t k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        if (r) {
+            k0 += PHILOX_W0;
+            k1 += PHILOX_W1;
+        }
+        uint64_t p0 = (uint64_t)PHILOX_M0 * c0;
+        uint64_t p1 = (uint64_t)PHILOX_M1 * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        uint32_t n1 = (uint32_t)p1;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        uint32_t n3 = (uint32_t)p0;
+        c0 = n0;
+        c1 = n1;
+        c2 = n2;
+        c3 = n3;
+    }
+    out[0] = c0;
+    out[1] = c1;
+    out[2] = c2;
+    out[3] = c3;
+}
+
+/* -------------------------------------------------------------- soft log */
+
+/* -ln(u), u = (w + 0.5) * 2^-32 = (2w + 1) * 2^-33.
+ * ln(m) for m = 2w+1 in [1, 2^33): m = 2^ex * f, f folded into (sqrt(2)/2, sqrt(2)],
+ * ln f = 2 atanh(s), s = (f-1)/(f+1), series to s^19. Fixed operation order. */
+double oracle_softlog_neg(uint32_t w) {
+    uint64_t m = 2u * (uint64_t)w + 1u;
+    int ex = 63 - __builtin_clzll(m);
+    double d = (double)m; /* exact: m < 2^33 */
+    union {
+        double f;
+        uint64_t u;
+    } sc;
+    sc.u = (uint64_t)(1023 - ex) << 52; /* 2^-ex, exact */
+    double f = d * sc.f;                /* exact, in [1, 2) */
+    if (f > 0x1.6a09e667f3bcdp+0) {
+        f = f * 0.5;
+        ex += 1;
+    }
+    double s = (f - 1.0) / (f + 1.0);
+    double z = s * s;
+    double r = 0x1.af286bca1af28p-5;     /* 1/19 */
+    r = r * z + 0x1.e1e1e1e1e1e1ep-5;    /* 1/17 */
+    r = r * z + 0x1.1111111111111p-4;    /* 1/15 */
+    r = r * z + 0x1.3b13b13b13b14p-4;    /* 1/13 */
+    r = r * z + 0x1.745d1745d1746p-4;    /* 1/11 */
+    r = r * z + 0x1.c71c71c71c71cp-4;    /* 1/9 */
+    r = r * z + 0x1.2492492492492p-3;    /* 1/7 */
+    r = r * z + 0x1.999999999999ap-3;    /* 1/5 */
+    r = r * z + 0x1.5555555555555p-2;    /* 1/3 */
+    double s2 = s + s;
+    double lnf = s2 + (s2 * z) * r;
+    return (double)(33 - ex) * 0x1.62e42fefa39efp-1 - lnf;
+}
+
+/* ------------------------------------------------------------ word stream */
+
+/* Per-event extra words: [w2, w3, blk1.x, blk1.y, blk1.z, blk1.w, blk2.x, ...]
+ * where blk j = Philox(ctr = (e, j, rid lo, rid hi)). */
+typedef struct {
+    uint32_t key[2];
+    uint32_t e, rid_lo, rid_hi;
+    uint32_t w2, w3;
+    uint32_t buf[4];
+    uint32_t blk;
+    uint32_t pos;
+} wstream;
+
+static uint32_t ws_next(wstream* s) {
+    uint32_t p = s->pos++;
+    if (p == 0) return s->w2;
+    if (p == 1) return s->w3;
+    uint32_t q = p - 2;
+    uint32_t j = q / 4 + 1;
+    if (j != s->blk) {
+        uint32_t ctr[4] = {s->e, j, s->rid_lo, s->rid_hi};
+        oracle_philox4x32_10(ctr, s->key, s->buf);
+        s->blk = j;
+    }
+    return s->buf[q % 4];
+}
+
+/* Uniform index in [0, L), L in [1, 2^32): Lemire multiply-shift with exact rejection
+ * (stands in for rand 0.8.5 gen_range(0..len)). */
+static uint32_t ws_index(wstream* s, uint32_t L) {
+    uint64_t m = (uint64_t)ws_next(s) * L;
+    uint32_t lo = (uint32_t)m;
+    if (lo < L) {
+        uint32_t thr = (uint32_t)(0u - L) % L;
+        while (lo < thr) {
+            m = (uint64_t)ws_next(s) * L;
+            lo = (uint32_t)m;
+        }
+    }
+    return (uint32_t)(m >> 32);
+}
+
+/* k1 ~ Binomial(n, 1/2) exactly: popcount of n fair bits taken from the stream. */
+static uint32_t ws_binomial_half(wstream* s, uint32_t n) {
+    uint32_t c = 0;
+    while (n >= 32) {
+        c += (uint32_t)__builtin_popcount(ws_next(s));
+        n -= 32;
+    }
+    if (n) c += (uint32_t)__builtin_popcount(ws_next(s) & ((1u << n) - 1u));
+    return c;
+}
+
+#define UNEVEN_FALSE 0
+#define UNEVEN_TRUE 1
+#define UNEVEN_TRUE_NO_NMINUS 2
+#define NO_UNEVEN_MAX_TRIES 4096
+
+/* Segregate::ecdna_segregation for n = 2k (src/segregation.rs:110-194). */
+static int segregate(wstream* s, int seg, uint32_t n, uint32_t* k1, int* uneven) {
+    switch (seg) {
+        case ECDNA_SEG_DETERMINISTIC: /* k1 = k2 = n/2, IsUneven::False (src/segregation.rs:142-155) */
+            *k1 = n / 2;
+            *uneven = UNEVEN_FALSE;
+            return 0;
+        case ECDNA_SEG_BINOMIAL: { /* k1 ~ Bin(n, 1/2); uneven iff k1==0 || k2==0 (:110-140) */
+            uint32_t x = ws_binomial_half(s, n);
+            *k1 = x;
+            *uneven = (x == 0 || x == n) ? UNEVEN_TRUE : UNEVEN_FALSE;
+            return 0;
+        }
+        case ECDNA_SEG_BINOMIAL_NO_UNEVEN: { /* redraw while uneven (:157-174) */
+            for (int t = 0; t < NO_UNEVEN_MAX_TRIES; ++t) {
+                uint32_t x = ws_binomial_half(s, n);
+                if (x != 0 && x != n) {
+                    *k1 = x;
+                    *uneven = UNEVEN_FALSE;
+                    return 0;
+                }
+            }
+            return ECDNA_REP_ERR_REJECTION;
+        }
+        case ECDNA_SEG_BINOMIAL_NO_NMINUS: { /* uneven relabelled (:176-194) */
+            uint32_t x = ws_binomial_half(s, n);
+            *k1 = x;
+            *uneven = (x == 0 || x == n) ? UNEVEN_TRUE_NO_NMINUS : UNEVEN_FALSE;
+            return 0;
+        }
+    }
+    return -1;
+}
+
+static void ws_init(wstream* s, uint64_t seed, uint64_t rid, uint32_t e, uint32_t w2, uint32_t w3) {
+    s->key[0] = (uint32_t)seed;
+    s->key[1] = (uint32_t)(seed >> 32);
+    s->e = e;
+    s->rid_lo = (uint32_t)rid;
+    s->rid_hi = (uint32_t)(rid >> 32);
+    s->w2 = w2;
+    s->w3 = w3;
+    s->blk = 0;
+    s->pos = 0;
+}
+
+static void event_block(uint64_t seed, uint64_t rid, uint32_t e, uint32_t w[4]) {
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t ctr[4] = {e, 0u, (uint32_t)rid, (uint32_t)(rid >> 32)};
+    oracle_philox4x32_10(ctr, key, w);
+}
+
+/* ---------------------------------------------------------- event kernels */
+
+/* Exponential::increase_nplus (src/proliferation.rs:25-111): pick-remove a uniform N+ cell
+ * (swap_remove), double its copies (checked: src/proliferation.rs:63-67), segregate, push
+ * [k1, k2] (False) or [k1+k2] (+1 N- for True). Returns 0 or an ecdna_rep_error_t; on error the
+ * distribution is unchanged. */
+static int prolif_nplus(uint16_t* row, uint64_t* len, uint64_t* nminus, uint64_t cap, wstream* ws,
+                        int seg, uint32_t* idx_out, uint32_t* k1_out, uint32_t* k2_out, int* uneven_out) {
+    uint64_t L = *len;
+    uint32_t i = ws_index(ws, (uint32_t)L);
+    uint32_t k = row[i];
+    if (k > 32767u) return ECDNA_REP_ERR_OVERFLOW;
+    uint32_t n = 2u * k;
+    uint32_t k1;
+    int uneven;
+    int err = segregate(ws, seg, n, &k1, &uneven);
+    if (err) return err;
+    if (uneven == UNEVEN_FALSE && L + 1 > cap) return ECDNA_REP_ERR_CELL_CAP;
+    row[i] = row[L - 1]; /* swap_remove(i) */
+    L -= 1;
+    if (uneven == UNEVEN_FALSE) {
+        row[L++] = (uint16_t)k1;
+        row[L++] = (uint16_t)(n - k1);
+    } else {
+        if (uneven == UNEVEN_TRUE) *nminus += 1;
+        row[L++] = (uint16_t)n;
+    }
+    *len = L;
+    *idx_out = i;
+    *k1_out = k1;
+    *k2_out = n - k1;
+    *uneven_out = uneven;
+    return 0;
+}
+
+/* CellDeath::decrease_nplus (src/proliferation.rs:126-133): gen_range + swap_remove. */
+static uint32_t death_nplus(uint16_t* row, uint64_t* len, wstream* ws) {
+    uint64_t L = *len;
+    uint32_t i = ws_index(ws, (uint32_t)L);
+    row[i] = row[L - 1];
+    *len = L - 1;
+    return i;
+}
+
+/* -------------------------------------------------------------- one run */
+
+typedef struct {
+    const ecdna_ssa_params_t* p;
+    ecdna_rep_summary_t* summaries;
+    uint16_t* rows;
+    uint64_t row_stride;
+    atomic_ullong next;
+    pthread_mutex_t mu;
+    uint64_t* hist;
+    ecdna_totals_t* totals;
+    int compat;
+} run_ctx;
+
+#define FNV_OFFSET 0xcbf29ce484222325ull
+#define FNV_PRIME 0x100000001b3ull
+
+static inline uint64_t fnv_fold(uint64_t h, uint64_t x) { return (h ^ x) * FNV_PRIME; }
+
+static void init_of_set(const ecdna_ssa_params_t* p, uint64_t set, const uint16_t** copies,
+                        uint64_t* nplus, uint64_t* nminus) {
+    if (p->init_set_offsets) {
+        *copies = p->init_copies + p->init_set_offsets[set];
+        *nplus = p->init_set_offsets[set + 1] - p->init_set_offsets[set];
+        *nminus = p->init_set_nminus ? p->init_set_nminus[set] : p->init_nminus;
+    } else {
+        *copies = p->init_copies;
+        *nplus = p->init_nplus;
+        *nminus = p->init_set_nminus ? p->init_set_nminus[set] : p->init_nminus;
+    }
+}
+
+/* One replicate: the sosa::simulate loop around advance_step (SURVEY.md App. A.3 / DESIGN.md §3.1). */
+static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16_t* row,
+                               ecdna_rep_summary_t* out) {
+    const uint64_t set = rid / p->reps_per_set;
+    const ecdna_rates_t rt = p->rates[set];
+    const int bd = p->process == ECDNA_BIRTH_DEATH;
+    const int f32t = (p->flags & ECDNA_FLAG_TIME_F32) != 0;
+    const int hash_on = (p->flags & ECDNA_FLAG_EVENT_HASH) != 0;
+    const uint64_t cells_mul = (bd && (p->flags & ECDNA_FLAG_BD_CAP_COMPAT)) ? 2u : 1u;
+
+    const uint16_t* init;
+    uint64_t nplus, nminus;
+    init_of_set(p, set, &init, &nplus, &nminus);
+    memcpy(row, init, nplus * sizeof(uint16_t));
+
+    memset(out, 0, sizeof(*out));
+    uint64_t h = FNV_OFFSET;
+    double t = 0.0;
+    float t32 = 0.0f;
+    const float max_t32 = (float)p->max_time;
+    uint32_t e = 0;
+    uint32_t stop = ECDNA_STOP_NONE, err = ECDNA_REP_OK;
+    uint64_t cnt[4] = {0, 0, 0, 0}, uneven_n = 0;
+
+    if (nplus == 0 && nminus == 0) { /* ensure!(!distribution.is_empty()) src/process.rs:88, 232 */
+        err = ECDNA_REP_ERR_EMPTY;
+        stop = ECDNA_STOP_ERROR;
+    }
+    while (!stop) {
+        if ((uint64_t)e >= p->max_iter) {
+            stop = ECDNA_STOP_MAX_ITER;
+            break;
+        }
+        if ((nminus + nplus) * cells_mul >= p->max_cells) {
+            stop = ECDNA_STOP_MAX_CELLS;
+            break;
+        }
+        if (f32t ? (t32 >= max_t32) : (t >= p->max_time)) {
+            stop = ECDNA_STOP_MAX_TIME;
+            break;
+        }
+        /* propensities rate_i * population_i, population = update_state's vector */
+        double a[4];
+        a[0] = (double)rt.b0 * (double)nminus;
+        a[1] = (double)rt.b1 * (double)nplus;
+        a[2] = bd ? (double)rt.d0 * (double)nminus : 0.0;
+        a[3] = bd ? (double)rt.d1 * (double)nplus : 0.0;
+        double c0 = a[0];
+        double c1 = c0 + a[1];
+        double c2 = c1 + a[2];
+        double a0 = c2 + a[3];
+        if (!(a0 > 0.0)) {
+            stop = ECDNA_STOP_ABSORBING;
+            break;
+        }
+        uint32_t w[4];
+        event_block(p->seed, rid, e, w);
+        /* direct method: channel by w1 against the cumulative propensities */
+        double target = (((double)w[1] + 0.5) * 0x1p-32) * a0;
+        int ch = target < c0 ? 0 : (target < c1 ? 1 : (target < c2 ? 2 : 3));
+        double tau = oracle_softlog_neg(w[0]) / a0;
+        wstream ws;
+        ws_init(&ws, p->seed, rid, e, w[2], w[3]);
+        uint64_t x = (uint64_t)ch;
+        switch (ch) {
+            case ECDNA_EV_PROLIF_NMINUS: /* increase_nminus (src/proliferation.rs:113-117) */
+                nminus += 1;
+                break;
+            case ECDNA_EV_PROLIF_NPLUS: {
+                uint32_t i, k1, k2;
+                int un;
+                int rc = prolif_nplus(row, &nplus, &nminus, p->cell_cap, &ws, p->segregation, &i, &k1, &k2, &un);
+                if (rc) {
+                    err = (uint32_t)rc;
+                    stop = ECDNA_STOP_ERROR;
+                    continue;
+                }
+                if (un != UNEVEN_FALSE) uneven_n += 1;
+                x |= ((uint64_t)k1 << 2) | ((uint64_t)i << 20);
+                break;
+            }
+            case ECDNA_EV_DEATH_NMINUS: /* decrease_nminus (src/proliferation.rs:135-139) */
+                nminus -= 1;
+                break;
+            default: { /* decrease_nplus (src/proliferation.rs:126-133) */
+                uint32_t i = death_nplus(row, &nplus, &ws);
+                x |= (uint64_t)i << 20;
+                break;
+            }
+        }
+        cnt[ch] += 1;
+        e += 1;
+        if (f32t)
+            t32 = t32 + (float)tau;
+        else
+            t = t + tau; /* self.time += reaction.time (src/process.rs:184, 336) */
+        if (hash_on) h = fnv_fold(h, x);
+    }
+    out->nminus = nminus;
+    out->nplus = nplus;
+    out->iters = e;
+    for (int c = 0; c < 4; ++c) out->events_by_type[c] = cnt[c];
+    out->uneven = uneven_n;
+    out->time = f32t ? (double)t32 : t;
+    out->event_hash = hash_on ? h : 0;
+    out->stop_reason = stop;
+    out->error = err;
+}
+
+/* from ssa_compat.c */
+void oracle_compat_simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16_t* row,
+                                      ecdna_rep_summary_t* out);
+
+static void accumulate(const ecdna_ssa_params_t* p, uint64_t rid, const uint16_t* row,
+                       const ecdna_rep_summary_t* s, uint64_t* hist, ecdna_totals_t* tot) {
+    const uint64_t set = rid / p->reps_per_set;
+    uint64_t* hb = hist + set * p->hist_bins;
+    const uint64_t last = p->hist_bins - 1;
+    hb[0] += s->nminus;
+    for (uint64_t j = 0; j < s->nplus; ++j) {
+        uint64_t k = row[j];
+        hb[k < last ? k : last] += 1;
+    }
+    ecdna_totals_t* t = tot + set;
+    t->replicates += 1;
+    t->events += s->iters;
+    for (int c = 0; c < 4; ++c) t->events_by_type[c] += s->events_by_type[c];
+    t->uneven += s->uneven;
+    t->nminus += s->nminus;
+    t->nplus += s->nplus;
+    t->stop_reasons[s->stop_reason] += 1;
+    t->errors += s->error != 0;
+}
+
+static void* worker(void* arg) {
+    run_ctx* c = (run_ctx*)arg;
+    const ecdna_ssa_params_t* p = c->p;
+    uint64_t nb = (uint64_t)p->n_param_sets * p->hist_bins;
+    uint64_t* hist = calloc(nb, sizeof(uint64_t));
+    ecdna_totals_t* tot = calloc(p->n_param_sets, sizeof(ecdna_totals_t));
+    uint16_t* scratch = c->rows ? NULL : malloc((size_t)(p->cell_cap ? p->cell_cap : 1) * sizeof(uint16_t));
+    for (;;) {
+        uint64_t i = atomic_fetch_add(&c->next, 1);
+        if (i >= p->n_replicates) break;
+        uint64_t rid = p->first_replicate + i;
+        uint16_t* row = c->rows ? c->rows + i * c->row_stride : scratch;
+        ecdna_rep_summary_t s;
+        if (c->compat)
+            oracle_compat_simulate_replicate(p, rid, row, &s);
+        else
+            simulate_replicate(p, rid, row, &s);
+        if (c->summaries) c->summaries[i] = s;
+        accumulate(p, rid, row, &s, hist, tot);
+    }
+    pthread_mutex_lock(&c->mu);
+    for (uint64_t b = 0; b < nb; ++b) c->hist[b] += hist[b];
+    for (uint32_t s = 0; s < p->n_param_sets; ++s) {
+        ecdna_totals_t* d = &c->totals[s];
+        const ecdna_totals_t* q = &tot[s];
+        d->replicates += q->replicates;
+        d->events += q->events;
+        for (int k = 0; k < 4; ++k) d->events_by_type[k] += q->events_by_type[k];
+        d->uneven += q->uneven;
+        d->nminus += q->nminus;
+        d->nplus += q->nplus;
+        for (int k = 0; k < 6; ++k) d->stop_reasons[k] += q->stop_reasons[k];
+        d->errors += q->errors;
+    }
+    pthread_mutex_unlock(&c->mu);
+    free(hist);
+    free(tot);
+    free(scratch);
+    return NULL;
+}
+
+/* Parameter checks — the same contract as the product (include/ecdna_ssa.h). */
+static int validate(const ecdna_ssa_params_t* p, uint64_t row_stride, int want_rows) {
+    if (!p || !p->rates || p->n_param_sets == 0 || p->reps_per_set == 0 || p->hist_bins < 2)
+        return ECDNA_E_INVALID;
+    if (p->process != ECDNA_PURE_BIRTH && p->process != ECDNA_BIRTH_DEATH) return ECDNA_E_INVALID;
+    if (p->segregation < 0 || p->segregation > 3) return ECDNA_E_INVALID;
+    if (p->max_iter > 0xffffffffull) return ECDNA_E_INVALID;
+    if (p->n_replicates && (p->first_replicate + p->n_replicates - 1) / p->reps_per_set >= p->n_param_sets)
+        return ECDNA_E_INVALID;
+    if (!p->init_copies && (p->init_nplus || p->init_set_offsets)) return ECDNA_E_INVALID;
+    uint64_t maxn = 0;
+    for (uint32_t s = 0; s < p->n_param_sets; ++s) {
+        const uint16_t* c;
+        uint64_t np, nm;
+        init_of_set(p, s, &c, &np, &nm);
+        if (np > maxn) maxn = np;
+        for (uint64_t j = 0; j < np; ++j)
+            if (c[j] == 0) return ECDNA_E_INVALID;
+        if (!p->init_set_offsets) break;
+    }
+    if (maxn > p->cell_cap) return ECDNA_E_INVALID;
+    if (want_rows && row_stride < p->cell_cap) return ECDNA_E_INVALID;
+    return ECDNA_OK;
+}
+
+static int run_pool(const ecdna_ssa_params_t* p, ecdna_rep_summary_t* out_summaries, uint64_t* out_hist,
+                    ecdna_totals_t* out_totals, uint16_t* out_rows, uint64_t row_stride, int n_threads,
+                    int compat) {
+    int rc = validate(p, row_stride, out_rows != NULL);
+    if (rc) return rc;
+    run_ctx c;
+    memset(&c, 0, sizeof(c));
+    c.p = p;
+    c.summaries = out_summaries;
+    c.rows = out_rows;
+    c.row_stride = row_stride;
+    atomic_init(&c.next, 0);
+    pthread_mutex_init(&c.mu, NULL);
+    uint64_t nb = (uint64_t)p->n_param_sets * p->hist_bins;
+    c.hist = calloc(nb, sizeof(uint64_t));
+    c.totals = calloc(p->n_param_sets, sizeof(ecdna_totals_t));
+    c.compat = compat;
+    if (n_threads <= 0) n_threads = (int)sysconf(_SC_NPROCESSORS_ONLN);
+    if (n_threads < 1) n_threads = 1;
+    if ((uint64_t)n_threads > p->n_replicates) n_threads = p->n_replicates ? (int)p->n_replicates : 1;
+    pthread_t* th = malloc(sizeof(pthread_t) * (size_t)n_threads);
+    for (int i = 1; i < n_threads; ++i) pthread_create(&th[i], NULL, worker, &c);
+    worker(&c);
+    for (int i = 1; i < n_threads; ++i) pthread_join(th[i], NULL);
+    free(th);
+    if (out_hist) memcpy(out_hist, c.hist, nb * sizeof(uint64_t));
+    if (out_totals) memcpy(out_totals, c.totals, p->n_param_sets * sizeof(ecdna_totals_t));
+    free(c.hist);
+    free(c.totals);
+    pthread_mutex_destroy(&c.mu);
+    return ECDNA_OK;
+}
+
+int oracle_run_philox(const ecdna_ssa_params_t* p, ecdna_rep_summary_t* out_summaries, uint64_t* out_hist,
+                      ecdna_totals_t* out_totals, uint16_t* out_rows, uint64_t row_stride, int n_threads) {
+    return run_pool(p, out_summaries, out_hist, out_totals, out_rows, row_stride, n_threads, 0);
+}
+
+int oracle_run_compat(const ecdna_ssa_params_t* p, ecdna_rep_summary_t* out_summaries, uint64_t* out_hist,
+                      ecdna_totals_t* out_totals, uint16_t* out_rows, uint64_t row_stride, int n_threads) {
+    return run_pool(p, out_summaries, out_hist, out_totals, out_rows, row_stride, n_threads, 1);
+}
+
+/* ------------------------------------------------------ single events */
+
+int oracle_increase_nplus(oracle_distr_t* d, int seg, uint64_t seed, uint64_t rid, uint32_t e, uint32_t* k1,
+                          uint32_t* k2, int* is_uneven) {
+    if (d->len == 0) return -1; /* pick_remove_random_nplus fails on no N+ cells (src/proliferation.rs:55-57) */
+    uint32_t w[4];
+    event_block(seed, rid, e, w);
+    wstream ws;
+    ws_init(&ws, seed, rid, e, w[2], w[3]);
+    uint32_t i;
+    return prolif_nplus(d->cells, &d->len, &d->nminus, d->cap, &ws, seg, &i, k1, k2, is_uneven);
+}
+
+int oracle_decrease_nplus(oracle_distr_t* d, uint64_t seed, uint64_t rid, uint32_t e) {
+    if (d->len == 0) return -1;
+    uint32_t w[4];
+    event_block(seed, rid, e, w);
+    wstream ws;
+    ws_init(&ws, seed, rid, e, w[2], w[3]);
+    death_nplus(d->cells, &d->len, &ws);
+    return 0;
+}
+
+int oracle_segregate(int seg, uint32_t n, uint64_t seed, uint64_t rid, uint32_t e, uint32_t* k1, uint32_t* k2,
+                     int* is_uneven) {
+    if (n < 2 || (n & 1u) || n > 65534u) return -1; /* DNACopySegregating::try_from (src/segregation.rs:28-40) */
+    uint32_t w[4];
+    event_block(seed, rid, e, w);
+    wstream ws;
+    ws_init(&ws, seed, rid, e, w[2], w[3]);
+    ws.pos = 1; /* segregation draws start at w3, after the cell pick's w2 */
+    int rc = segregate(&ws, seg, n, k1, is_uneven);
+    if (!rc) *k2 = n - *k1;
+    return rc;
+}

@@ -1,0 +1,92 @@
+/*
+ * ssa_oracle.h — TEST INFRASTRUCTURE ONLY. CPU restatement of the reference's
+ * hot path (fraterenz/ecdna-evo v0.26.0: sosa::simulate driving
+ * PureBirth/BirthDeath::advance_step, Exponential/CellDeath and the Segregate
+ * rules), used as the parity checker for the HIP engine and as the timed CPU
+ * baseline in bench.py. Never linked into, or called by, the product library
+ * (ecdna-evo_amd/): only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg load it.
+ *
+ * Two modes:
+ *   philox  (ssa_oracle.c) — the engine's own draw mapping:
+ *           bit-exact with the GPU (event sequence, rows, time, hash).
+ *   compat  (ssa_compat.c) — the reference's own samplers as reconstructed in
+ *           ChaCha8 streams seed*10+i, first-reaction method,
+ *           gen_range + swap_remove, rand_distr Exp1 ziggurat and Binomial
+ *           (BINV/BTPE). The crates (sosa 3.0.3, ecdna-lib 3.0.2,
+ *           rand 0.8.5, rand_chacha 0.3.1, rand_distr 0.4.3; Cargo.lock:423-438,
+ *           802-839, 944-955) are not vendored and no Rust toolchain exists
+ *           here, so compat is matched to the reference in distribution only
+ *           ("parity unpinned" seed-for-seed).
+ */
+#ifndef ECDNA_SSA_ORACLE_H
+#define ECDNA_SSA_ORACLE_H
+
+#include <stdint.h>
+
+#include "../include/ecdna_ssa.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- primitives (philox mode) ---- */
+void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+/* -ln((w + 0.5) * 2^-32) by the engine's fixed-operation-order software log. */
+double oracle_softlog_neg(uint32_t w);
+
+/* ---- whole runs ---- */
+/* Same contract as ecdna_ssa_run (include/ecdna_ssa.h) with host buffers; out_rows, if given,
+ * receives [n_replicates][row_stride] final N+ rows. n_threads <= 0: all hardware threads. */
+int oracle_run_philox(const ecdna_ssa_params_t* p, ecdna_rep_summary_t* out_summaries,
+                      uint64_t* out_hist, ecdna_totals_t* out_totals, uint16_t* out_rows,
+                      uint64_t row_stride, int n_threads);
+/* Reference-semantics CPU path: stream of global replicate r is seed*10 + r (src/main.rs:56-58,
+ * 213-215). Time is always accumulated in f32 like process.time (src/process.rs:184, 336);
+ * ECDNA_FLAG_EVENT_HASH is honoured, ECDNA_FLAG_TIME_F32 is implied. */
+int oracle_run_compat(const ecdna_ssa_params_t* p, ecdna_rep_summary_t* out_summaries,
+                      uint64_t* out_hist, ecdna_totals_t* out_totals, uint16_t* out_rows,
+                      uint64_t row_stride, int n_threads);
+
+/* ---- single-event API (mirrors the reference's unit-tested functions) ---- */
+/* EcDNADistribution restated: n- plus one u16 per N+ cell. */
+typedef struct {
+    uint16_t* cells;
+    uint64_t len;
+    uint64_t cap;
+    uint64_t nminus;
+} oracle_distr_t;
+
+/* Exponential::increase_nplus (src/proliferation.rs:25-111) with the philox draws of event e of
+ * replicate rid. Returns 0, or an ecdna_rep_error_t. *is_uneven: 0 False, 1 True,
+ * 2 TrueWithoutNMinusIncrease (src/segregation.rs:50-57). */
+int oracle_increase_nplus(oracle_distr_t* d, int seg, uint64_t seed, uint64_t rid, uint32_t e,
+                          uint32_t* k1, uint32_t* k2, int* is_uneven);
+/* CellDeath::decrease_nplus (src/proliferation.rs:126-133). Returns 0 or an error. */
+int oracle_decrease_nplus(oracle_distr_t* d, uint64_t seed, uint64_t rid, uint32_t e);
+/* Segregate::ecdna_segregation for n = 2k copies (src/segregation.rs:75-84). Returns 0 or
+ * ECDNA_REP_ERR_REJECTION; n must be even and >= 2 (DNACopySegregating, src/segregation.rs:28-40),
+ * else returns -1. */
+int oracle_segregate(int seg, uint32_t n, uint64_t seed, uint64_t rid, uint32_t e, uint32_t* k1,
+                     uint32_t* k2, int* is_uneven);
+
+/* ---- compat-mode primitives ---- */
+/* ChaCha block function with `rounds` rounds over the 16-word state in[16] (RFC 7539 layout). */
+void oracle_chacha_block(const uint32_t in[16], uint32_t out[16], int rounds);
+/* rand_core 0.6 seed_from_u64: the 32-byte ChaCha key (8 words) expanded by PCG32. */
+void oracle_chacha_seed_from_u64(uint64_t seed, uint32_t key[8]);
+/* Opaque ChaCha8Rng (rand_chacha 0.3.1) and its samplers, for distribution tests. */
+typedef struct oracle_chacha oracle_chacha;
+oracle_chacha* oracle_chacha_new(uint64_t seed, uint64_t stream);
+void oracle_chacha_free(oracle_chacha* r);
+uint32_t oracle_chacha_next_u32(oracle_chacha* r);
+uint64_t oracle_chacha_next_u64(oracle_chacha* r);
+uint64_t oracle_compat_gen_range(oracle_chacha* r, uint64_t n);   /* rand 0.8.5 gen_range(0..n) */
+double oracle_compat_exp1(oracle_chacha* r);                        /* rand_distr Exp1 (ziggurat) */
+uint64_t oracle_compat_binomial(oracle_chacha* r, uint64_t n, double p); /* rand_distr Binomial */
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,62 @@
+"""Parity cases shared by the GPU parity tests and the golden-fixture generator.
+
+Each case is a small RunSpec the CPU oracle finishes in well under a second. Together they cover
+both processes, all four segregation rules, f32/f64 time, the birth-death cap-compat flag, single-
+and multi-set (ABC) runs, non-default initial distributions, replicate-id offsets (sharding) and
+every stop reason and per-replicate error the engine reports.
+"""
+from ecdna_evo_amd import abi
+
+H = abi.FLAG_EVENT_HASH
+
+BD_RATES = ((1.0, 1.5, 0.3, 0.3),)  # C3 shape
+
+
+def cases():
+    c = {}
+    # C1 shape: pure birth + binomial to 1e3 cells, seed 42 (BASELINE.json configs[0])
+    c["pb_binomial_c1"] = abi.RunSpec(seed=42, n_replicates=64, max_cells=1000, flags=H)
+    for name, seg in abi.SEGREGATION_NAMES.items():
+        c[f"pb_{name}"] = abi.RunSpec(seed=7, segregation=seg, n_replicates=48, max_cells=600,
+                                      init={3: 2, 8: 1}, flags=H)
+        c[f"bd_{name}"] = abi.RunSpec(seed=11, segregation=seg, process=abi.BIRTH_DEATH, rates=BD_RATES,
+                                      n_replicates=48, max_cells=800, flags=H)
+    c["pb_f32_time"] = abi.RunSpec(seed=5, n_replicates=32, max_cells=500, flags=H | abi.FLAG_TIME_F32)
+    c["bd_f32_time"] = abi.RunSpec(seed=5, process=abi.BIRTH_DEATH, rates=BD_RATES, n_replicates=32,
+                                   max_cells=500, flags=H | abi.FLAG_TIME_F32)
+    c["bd_cap_compat"] = abi.RunSpec(seed=9, process=abi.BIRTH_DEATH, rates=BD_RATES, n_replicates=32,
+                                     max_cells=1000, flags=H | abi.FLAG_BD_CAP_COMPAT)
+    c["bd_selection"] = abi.RunSpec(seed=3, process=abi.BIRTH_DEATH, rates=((1.0, 2.0, 0.5, 0.1),),
+                                    n_replicates=32, max_cells=1500, init={1: 4, 0: 2}, flags=H)
+    # turnover: d close to b, 1000 initial cells, time-capped (C5 shape, scaled down)
+    c["bd_turnover"] = abi.RunSpec(seed=13, process=abi.BIRTH_DEATH, rates=((1.0, 1.0, 0.9, 0.9),),
+                                   n_replicates=16, max_cells=1_300, max_time=3.0, init={1: 1000}, flags=H)
+    # extinction-prone: death > birth -> Absorbing
+    c["bd_extinction"] = abi.RunSpec(seed=17, process=abi.BIRTH_DEATH, rates=((1.0, 1.0, 1.5, 1.5),),
+                                     n_replicates=64, max_cells=400, init={2: 3}, flags=H)
+    # ABC shape: 4 parameter sets x 8 replicates, per-set initial distributions (C4, scaled down)
+    c["abc_sets"] = abi.RunSpec(
+        seed=42, process=abi.BIRTH_DEATH, segregation=abi.SEG_BINOMIAL,
+        rates=((1.0, 1.0, 0.1, 0.1), (1.0, 1.5, 0.1, 0.1), (1.0, 2.0, 0.3, 0.2), (1.0, 2.5, 0.0, 0.4)),
+        reps_per_set=8, n_replicates=32, max_cells=700, hist_bins=257,
+        init_per_set=[{1: 1}, {2: 1}, {4: 1, 0: 3}, {8: 2}], flags=H)
+    # replicate-id offset: a shard of a bigger run
+    c["shard_offset"] = abi.RunSpec(seed=42, first_replicate=1000, n_replicates=40, max_cells=700,
+                                    reps_per_set=100000, flags=H)
+    # large copy numbers: n = 2k > 32 takes the multi-block popcount path
+    c["big_copies"] = abi.RunSpec(seed=21, n_replicates=24, max_cells=300, init={40: 2, 300: 1, 5000: 1},
+                                  hist_bins=64, flags=H)
+    c["big_copies_no_uneven"] = abi.RunSpec(seed=22, segregation=abi.SEG_BINOMIAL_NO_UNEVEN, n_replicates=24,
+                                            max_cells=300, init={17: 2, 64: 1}, flags=H)
+    # stop reasons and errors
+    c["max_iter"] = abi.RunSpec(seed=1, n_replicates=16, max_cells=10_000, max_iter=137, flags=H)
+    c["max_time"] = abi.RunSpec(seed=2, n_replicates=16, max_cells=100_000, max_time=2.5, cell_cap=4096, flags=H)
+    c["overflow"] = abi.RunSpec(seed=3, n_replicates=8, max_cells=50, init={32768: 1, 1: 1}, flags=H)
+    c["no_overflow_edge"] = abi.RunSpec(seed=3, segregation=abi.SEG_DETERMINISTIC, n_replicates=8, max_cells=50,
+                                        init={32767: 1}, flags=H)
+    c["cell_cap_error"] = abi.RunSpec(seed=4, n_replicates=8, max_cells=5000, cell_cap=100, flags=H)
+    c["empty_init"] = abi.RunSpec(seed=5, n_replicates=4, max_cells=100, init={}, flags=H)
+    c["nminus_only"] = abi.RunSpec(seed=6, n_replicates=4, max_cells=100, init={0: 5}, flags=H)
+    c["already_full"] = abi.RunSpec(seed=6, n_replicates=4, max_cells=3, init={1: 3}, flags=H)
+    c["no_hash"] = abi.RunSpec(seed=42, n_replicates=16, max_cells=500, flags=0)
+    return c
