@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Benchmark: Gillespie reaction-events/s of the MI355X SSA engine (BASELINE.json metric).
+
+Workload (N=1 line = BASELINE.json configs[2], "C3"): 2^20 independent replicates per GPU of the
+reference's birth-death process (b0=1, b1=1.5, d0=d1=0.3, Binomial segregation, initial {1: 1},
+stop at 1e4 cells or t = floor(log2(1e4)+4) = 17 years), seed 42. Weak scaling: rank g runs the
+global replicate ids [g*2^20, (g+1)*2^20) — per-GPU work is fixed as N grows — and the only
+collective is one all-reduce of the copy-number histogram + totals per step (RCCL over xGMI).
+
+One step = one full run of the hot path on every GPU: zero outputs, the persistent SSA stepper
+kernel over all 2^20 replicates, the histogram kernel, and (N>1) the all-reduce. Inputs are
+resident in HBM before the timed region.
+
+Extra JSON fields:
+  roofline      — the stepper kernel against HBM: algorithmic bytes per launch over
+                  its average duration (HIP events on the launch stream), vs 8 TB/s; `traffic` =
+                  measured HBM bytes per launch from the committed rocprofv3 PMC summary, if present.
+  cpu_baseline  — the reference-semantics CPU restatement (oracle/, ChaCha8 + first-reaction +
+                  BTPE, "port") on a bounded sample of the same workload, rank 0 at N=1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "ecdna-evo_amd"))
+
+import torch  # noqa: E402  (first: one HIP runtime for torch and the engine)
+import torch.distributed as dist  # noqa: E402
+
+from ecdna_evo_amd import abi, engine  # noqa: E402
+
+METRIC = "Gillespie reaction-events/sec at 2^20 replicates, 1/2/4/8 MI355X"
+REPS_PER_GPU = 1 << 20
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 TB/s measured copy)
+# algorithmic bytes per event: per-cell u16 row with swap_remove
+B_PROLIF_EVEN, B_PROLIF_UNEVEN, B_DEATH_NPLUS = 10, 8, 6
+B_SUMMARY = 88
+
+
+def workload_spec(first: int, n: int, total: int, seed: int = 42, device: int = 0) -> abi.RunSpec:
+    return abi.RunSpec(process=abi.BIRTH_DEATH, segregation=abi.SEG_BINOMIAL, rates=((1.0, 1.5, 0.3, 0.3),),
+                       reps_per_set=total, seed=seed, first_replicate=first, n_replicates=n, max_cells=10_000,
+                       hist_bins=1025, flags=0, device=device)
+
+
+def algorithmic_bytes(words, n_reps: int, init_cells: int = 1) -> int:
+    """words: one ecdna_totals_t as 16 u64 (replicates, events, events_by_type[4], uneven, ...)."""
+    uneven = int(words[6])
+    even = int(words[2 + abi.EV_PROLIF_NPLUS]) - uneven
+    return (B_PROLIF_EVEN * even + B_PROLIF_UNEVEN * uneven + B_DEATH_NPLUS * int(words[2 + abi.EV_DEATH_NPLUS])
+            + n_reps * (2 * init_cells + B_SUMMARY))
+
+
+def load_traffic(n_gpus: int):
+    """Measured HBM bytes per stepper launch (rocprofv3 PMC, corrected; profiles/pmc_c3.json)."""
+    p = os.path.join(REPO, "profiles", "pmc_c3.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(threads: int):
+    """Reference-semantics CPU path (oracle compat mode) timed on a bounded sample of the workload."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # test infrastructure: the CPU baseline only
+
+    t0 = time.time()
+    probe = workload_spec(0, 1024, REPS_PER_GPU)
+    r = oracle.run(probe, mode="compat", n_threads=threads)
+    dt = max(time.time() - t0, 1e-3)
+    target_s = float(os.environ.get("ECDNA_BENCH_CPU_SECONDS", "10"))
+    n = int(min(REPS_PER_GPU, max(1024, 1024 * target_s / dt)))
+    spec = workload_spec(0, n, REPS_PER_GPU)
+    t0 = time.time()
+    r = oracle.run(spec, mode="compat", n_threads=threads)
+    dt = time.time() - t0
+    ev = int(r.totals["events"].sum())
+    return {"value": ev / dt, "unit": "events/s", "cores": threads, "kind": "port",
+            "sample": f"C3 shape, replicates 0..{n - 1} of 2^20 ({ev} events, {dt:.1f} s wall), "
+                      f"oracle compat mode (ChaCha8 streams seed*10+i, first-reaction, BTPE), "
+                      f"{threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--reps-per-gpu", type=int, default=REPS_PER_GPU)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    n_gpus = world
+    reps = args.reps_per_gpu
+    total = reps * n_gpus
+
+    spec = workload_spec(rank * reps, reps, total, device=local if world > 1 else 0)
+    ctx = engine.Context(spec)
+    hist = torch.zeros(spec.hist_bins, dtype=torch.int64, device="cuda")
+    tot = torch.zeros(16, dtype=torch.int64, device="cuda")
+    ctx.set_outputs(hist.data_ptr(), tot.data_ptr())
+    torch_stream = torch.cuda.Stream()
+    torch.cuda.set_stream(torch_stream)  # torch ops and the engine's kernels share this stream
+    stream = torch_stream.cuda_stream
+
+    tot_local = torch.zeros_like(tot)
+
+    def step():
+        ctx.launch(stream)
+        tot_local.copy_(tot)  # this GPU's totals, before the reduction
+        if world > 1:
+            dist.all_reduce(hist)
+            dist.all_reduce(tot)
+
+    for _ in range(args.warmup):
+        step()
+        ctx.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kernel_ms, hist_ms = [], []
+    for _ in range(args.steps):
+        step()
+        s_ms, h_ms = ctx.sync()
+        kernel_ms.append(s_ms)
+        hist_ms.append(h_ms)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+
+    local_words = tot_local.cpu().numpy()
+    local_events = int(local_words[1])
+    local_alg = algorithmic_bytes(local_words, reps)
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    ev = torch.tensor([local_events], dtype=torch.int64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(ev)
+    elapsed = float(t.item())
+    events_per_step = int(ev.item())
+    # the all-reduced histogram must account for every cell of every replicate
+    tot_host = tot.cpu().numpy()
+    assert int(tot_host[0]) == total, f"all-reduced totals count {int(tot_host[0])} replicates, expected {total}"
+    assert int(tot_host[1]) == events_per_step
+
+    if rank == 0:
+        avg_kernel_s = sum(kernel_ms) / len(kernel_ms) * 1e-3
+        achieved = local_alg / avg_kernel_s / 1e9
+        traffic = load_traffic(n_gpus)
+        cpu = None
+        if n_gpus == 1 and not args.no_cpu_baseline:
+            threads = int(os.environ.get("ECDNA_BENCH_CPU_THREADS", "0")) or min(16, os.cpu_count() or 1)
+            cpu = cpu_baseline(threads)
+        chunk, lanes = ctx.geometry()
+        line = {
+            "metric": METRIC,
+            "value": events_per_step * args.steps / elapsed,
+            "unit": "events/s",
+            "n_gpus": n_gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u16+f64",
+            "data": "synthetic",
+            "config": {
+                "workload": "C3 (BASELINE.json configs[2]): 2^20 replicates/GPU, birth-death b0=1 b1=1.5 "
+                            "d0=d1=0.3, binomial segregation, init {1:1}, stop 1e4 cells or t=17, seed 42",
+                "replicates_per_gpu": reps,
+                "replicates_total": total,
+                "events_per_step": events_per_step,
+                "parallelism": f"replicas{n_gpus} (replicate-id shards, 1 RCCL all-reduce of the histogram)",
+                "grid_lanes": lanes,
+                "kernel_ms_avg": avg_kernel_s * 1e3,
+                "hist_kernel_ms_avg": sum(hist_ms) / len(hist_ms),
+                "kernel_events_per_s_per_gpu": local_events / avg_kernel_s,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -116,7 +116,6 @@ struct ecdna_ssa_ctx {
     ecdna_totals_t* d_tot_own = nullptr;
     uint64_t* d_hist = nullptr;
     ecdna_totals_t* d_tot = nullptr;
-    hipStream_t own_stream = nullptr;
     hipStream_t last_stream = nullptr;
     std::vector<Chunk> chunks;
     bool launched = false;
@@ -157,7 +156,6 @@ void free_ctx(ecdna_ssa_ctx* c) {
     (void)hipFree(c->d_heads);
     (void)hipFree(c->d_hist_own);
     (void)hipFree(c->d_tot_own);
-    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
 
@@ -232,7 +230,6 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
     hipDeviceProp_t prop;
     CTX_TRY(hipGetDeviceProperties(&prop, c->device));
     c->cus = prop.multiProcessorCount;
-    CTX_TRY(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
 
     // inputs
     std::vector<float4> r4(p->n_param_sets);
@@ -315,7 +312,7 @@ int ecdna_ssa_ctx_set_outputs(ecdna_ssa_ctx* c, uint64_t* d_hist, ecdna_totals_t
 int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
     if (!c) return fail(ECDNA_E_INVALID, "ctx is NULL");
     HIP_TRY(hipSetDevice(c->device));
-    hipStream_t st = stream ? (hipStream_t)stream : c->own_stream;
+    hipStream_t st = (hipStream_t)stream;  // NULL = the default (null) stream
     const ecdna_ssa_params_t& p = c->p;
     const uint64_t nb = (uint64_t)p.n_param_sets * p.hist_bins;
     HIP_TRY(hipMemsetAsync(c->d_hist, 0, nb * sizeof(uint64_t), st));

@@ -179,7 +179,7 @@ int ecdna_ssa_device_count(void);
 /* One-shot: runs every replicate of *p on device p->device and copies the results to HOST buffers
  * (each may be NULL): out_summaries[n_replicates] (replicate first_replicate + i at index i),
  * out_hist[n_param_sets * hist_bins] (zeroed, then filled), out_totals[n_param_sets].
- * stream: a hipStream_t, or NULL for a private stream. Blocks until done. */
+ * stream: a hipStream_t, or NULL for the default (null) stream. Blocks until done. */
 int ecdna_ssa_run(const ecdna_ssa_params_t* p, ecdna_rep_summary_t* out_summaries,
                   uint64_t* out_hist, ecdna_totals_t* out_totals, void* stream);
 
@@ -191,8 +191,8 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out);
 /* Use caller-owned DEVICE buffers for the histogram [n_param_sets*hist_bins] u64 and totals
  * [n_param_sets] (e.g. tensors later all-reduced over RCCL). NULL keeps the internal buffer. */
 int ecdna_ssa_ctx_set_outputs(ecdna_ssa_ctx* c, uint64_t* d_hist, ecdna_totals_t* d_totals);
-/* Enqueue one full run on `stream` (NULL = the context's stream): zero hist/totals, SSA kernel over
- * all replicates (in memory-bounded chunks), histogram kernel. Asynchronous. */
+/* Enqueue one full run on `stream` (a hipStream_t; NULL = the default stream): zero hist/totals, SSA
+ * kernel over all replicates (in memory-bounded chunks), histogram kernel. Asynchronous. */
 int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream);
 /* Block until the last launch finished; returns its device time in ms (HIP events on the launch
  * stream): ssa_ms = SSA stepper kernels only, hist_ms = histogram/summary kernels. Either may be NULL. */

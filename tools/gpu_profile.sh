@@ -1,0 +1,20 @@
+#!/bin/bash
+# One GPU session: bench (N=1), rocprofv3 kernel-trace stats of the same command, PMC passes
+# (FETCH_SIZE and WRITE_SIZE in separate passes) of a 1-step bench and of the calibration program.
+# Usage: bash tools/gpu_profile.sh <round-tag>
+set -euo pipefail
+TAG=${1:-r01}
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/prof_$TAG
+mkdir -p $O
+timeout -k 10 400 python3 bench.py --steps 3 --warmup 1 > $O/bench.json 2> $O/bench.err
+echo "bench done" 
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/kt -o kt -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/kt.log 2>&1
+echo "kernel trace done"
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $O/pmc_fetch -o pmc -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > $O/pmc_fetch.log 2>&1
+echo "pmc fetch done"
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $O/pmc_write -o pmc -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > $O/pmc_write.log 2>&1
+echo "pmc write done"
+timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $O/calib_fetch -o pmc -- tools/bin/pmc_calib > $O/calib_fetch.log 2>&1
+timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $O/calib_write -o pmc -- tools/bin/pmc_calib > $O/calib_write.log 2>&1
+echo "calib done"
