@@ -30,7 +30,7 @@ sys.path.insert(0, os.path.join(REPO, "ecdna-evo_amd"))
 import torch  # noqa: E402  (first: one HIP runtime for torch and the engine)
 import torch.distributed as dist  # noqa: E402
 
-from ecdna_evo_amd import abi, engine  # noqa: E402
+from ecdna_evo_amd import abi, engine, shard  # noqa: E402
 
 METRIC = "Gillespie reaction-events/sec at 2^20 replicates, 1/2/4/8 MI355X"
 REPS_PER_GPU = 1 << 20
@@ -108,7 +108,8 @@ def main():
     reps = args.reps_per_gpu
     total = reps * n_gpus
 
-    spec = workload_spec(rank * reps, reps, total, device=local if world > 1 else 0)
+    first, n = shard.weak_range(rank, reps)
+    spec = workload_spec(first, n, total, device=local if world > 1 else 0)
     ctx = engine.Context(spec)
     hist = torch.zeros(spec.hist_bins, dtype=torch.int64, device="cuda")
     tot = torch.zeros(16, dtype=torch.int64, device="cuda")
@@ -123,8 +124,7 @@ def main():
         ctx.launch(stream)
         tot_local.copy_(tot)  # this GPU's totals, before the reduction
         if world > 1:
-            dist.all_reduce(hist)
-            dist.all_reduce(tot)
+            shard.reduce_outputs(hist, tot)
 
     for _ in range(args.warmup):
         step()

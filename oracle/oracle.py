@@ -55,6 +55,10 @@ def lib():
     L.oracle_increase_nplus.restype = C.c_int
     L.oracle_decrease_nplus.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32]
     L.oracle_decrease_nplus.restype = C.c_int
+    L.oracle_increase_nminus.argtypes = [C.c_void_p]
+    L.oracle_increase_nminus.restype = C.c_int
+    L.oracle_decrease_nminus.argtypes = [C.c_void_p]
+    L.oracle_decrease_nminus.restype = C.c_int
     L.oracle_segregate.argtypes = [C.c_int, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32,
                                    P(C.c_uint32), P(C.c_uint32), P(C.c_int)]
     L.oracle_segregate.restype = C.c_int
@@ -153,6 +157,17 @@ class Distribution:
 
     def decrease_nplus(self, seed: int, rid: int, e: int) -> int:
         return lib().oracle_decrease_nplus(C.byref(self.d), seed, rid, e)
+
+    def increase_nminus(self) -> int:
+        return lib().oracle_increase_nminus(C.byref(self.d))
+
+    def decrease_nminus(self) -> int:
+        return lib().oracle_decrease_nminus(C.byref(self.d))
+
+    def mean(self) -> float:
+        # EcDNADistribution::compute_mean: mean copy number over all cells, N- included
+        total = self.nminus + self.nplus
+        return float(self.cells().astype(np.float64).sum() / total) if total else float("nan")
 
 
 def segregate(seg: int, n: int, seed: int, rid: int, e: int):

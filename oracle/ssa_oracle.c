@@ -556,6 +556,17 @@ int oracle_decrease_nplus(oracle_distr_t* d, uint64_t seed, uint64_t rid, uint32
     return 0;
 }
 
+int oracle_increase_nminus(oracle_distr_t* d) {
+    d->nminus += 1;
+    return 0;
+}
+
+int oracle_decrease_nminus(oracle_distr_t* d) {
+    if (d->nminus == 0) return -1;
+    d->nminus -= 1;
+    return 0;
+}
+
 int oracle_segregate(int seg, uint32_t n, uint64_t seed, uint64_t rid, uint32_t e, uint32_t* k1, uint32_t* k2,
                      int* is_uneven) {
     if (n < 2 || (n & 1u) || n > 65534u) return -1; /* DNACopySegregating::try_from (src/segregation.rs:28-40) */

@@ -64,6 +64,10 @@ int oracle_increase_nplus(oracle_distr_t* d, int seg, uint64_t seed, uint64_t ri
                           uint32_t* k1, uint32_t* k2, int* is_uneven);
 /* CellDeath::decrease_nplus (src/proliferation.rs:126-133). Returns 0 or an error. */
 int oracle_decrease_nplus(oracle_distr_t* d, uint64_t seed, uint64_t rid, uint32_t e);
+/* Exponential::increase_nminus (src/proliferation.rs:113-117) and CellDeath::decrease_nminus
+ * (src/proliferation.rs:135-139). decrease returns -1 when there is no N- cell. */
+int oracle_increase_nminus(oracle_distr_t* d);
+int oracle_decrease_nminus(oracle_distr_t* d);
 /* Segregate::ecdna_segregation for n = 2k copies (src/segregation.rs:75-84). Returns 0 or
  * ECDNA_REP_ERR_REJECTION; n must be even and >= 2 (DNACopySegregating, src/segregation.rs:28-40),
  * else returns -1. */

@@ -4,7 +4,8 @@ import sys
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for p in (os.path.join(REPO, "ecdna-evo_amd"), os.path.join(REPO, "oracle"), REPO):
+for p in (os.path.join(REPO, "ecdna-evo_amd"), os.path.join(REPO, "oracle"), REPO,
+          os.path.join(REPO, "tests", "golden")):
     if p not in sys.path:
         sys.path.insert(0, p)
 

@@ -1,0 +1,133 @@
+"""GPU tests at BASELINE.json's full sizes, through size-independent properties, plus the
+reference-semantics KS comparison (BASELINE.json north_star: KS < 0.01).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from ecdna_evo_amd import abi
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+KS_TOL = 0.01  # north_star: KS distance < 0.01 on the final copy-number histogram
+
+
+def _ks(h1, h2):
+    c1 = np.cumsum(h1.astype(np.float64)) / h1.sum()
+    c2 = np.cumsum(h2.astype(np.float64)) / h2.sum()
+    return float(np.abs(c1 - c2).max())
+
+
+def c2_spec(**kw):
+    d = dict(seed=42, n_replicates=65536, max_cells=10_000, hist_bins=1025, flags=0)
+    d.update(kw)
+    return abi.RunSpec(**d)
+
+
+def c3_spec(first=0, n=1 << 20, **kw):
+    d = dict(seed=42, process=abi.BIRTH_DEATH, rates=((1.0, 1.5, 0.3, 0.3),), reps_per_set=1 << 20,
+             first_replicate=first, n_replicates=n, max_cells=10_000, hist_bins=1025, flags=0)
+    d.update(kw)
+    return abi.RunSpec(**d)
+
+
+def _invariants(res, spec):
+    s, h, t = res.summaries, res.hist, res.totals
+    assert h[:, 0].sum() == s["nminus"].sum()
+    assert h[:, 1:].sum() == s["nplus"].sum()
+    assert np.all(s["iters"] == s["events_by_type"].sum(axis=1))
+    assert int(t["events"].sum()) == int(s["iters"].sum())
+    assert int(t["replicates"].sum()) == len(s)
+    assert np.all(s["error"] == 0)
+    assert np.all(np.bincount(s["stop_reason"], minlength=6) == t["stop_reasons"].sum(axis=0))
+
+
+@pytest.mark.gpu
+def test_c2_ks_against_reference_semantics(engine_mod):
+    """C2 shape (65,536 replicates, pure birth + binomial to 1e4 cells, seed 42) on the GPU vs the
+    committed reference-semantics fixture (ChaCha8 + first-reaction + BTPE, tests/golden/)."""
+    g = np.load(os.path.join(GOLDEN, "c2_compat_seed42.npz"))
+    r = engine_mod.run(c2_spec())
+    _invariants(r, c2_spec())
+    ks = _ks(r.hist[0], g["hist"])
+    assert ks < KS_TOL, ks
+    # per-replicate law of the N- fraction (two-sample KS on replicates, not cells)
+    from scipy import stats
+
+    fa = r.summaries["nminus"] / (r.summaries["nminus"] + r.summaries["nplus"])
+    fb = g["nminus"] / (g["nminus"] + g["nplus"]).astype(np.float64)
+    assert stats.ks_2samp(fa, fb).pvalue > 1e-4
+
+
+@pytest.mark.gpu
+def test_c2_pure_birth_exact_event_counts(engine_mod):
+    r = engine_mod.run(c2_spec())
+    s = r.summaries
+    full = s["stop_reason"] == abi.STOP_MAX_CELLS
+    assert full.mean() > 0.99
+    assert np.all(s["iters"][full] == 10_000 - 1)
+    assert np.all(s["stop_reason"][~full] == abi.STOP_MAX_TIME)
+
+
+@pytest.mark.gpu
+def test_c3_full_size_properties_and_shard_identity(engine_mod):
+    """C3 at 2^20 replicates: invariants, and the two halves run as separate shards (global ids)
+    reproduce the full run's summaries and histogram bit for bit (the 1-GPU == N-GPU identity)."""
+    full = engine_mod.run(c3_spec())
+    _invariants(full, c3_spec())
+    half = 1 << 19
+    a = engine_mod.run(c3_spec(0, half))
+    b = engine_mod.run(c3_spec(half, half))
+    for f in full.summaries.dtype.names:
+        np.testing.assert_array_equal(np.concatenate([a.summaries[f], b.summaries[f]]), full.summaries[f])
+    np.testing.assert_array_equal(a.hist + b.hist, full.hist)
+    # extinction probability of a birth-death process from one N+ cell ~ d1/b1 = 0.2 (k=1 start
+    # loses its ecDNA only by uneven division, whose N- daughters then die out with prob d0/b0)
+    ext = np.mean(full.summaries["stop_reason"] == abi.STOP_ABSORBING)
+    assert 0.15 < ext < 0.35
+
+
+@pytest.mark.gpu
+def test_c3_matches_oracle_on_a_sample(engine_mod, oracle_mod):
+    """Replicates 0..4095 of the C3 run, checked against the oracle bit for bit (hash on)."""
+    spec = c3_spec(0, 4096, flags=abi.FLAG_EVENT_HASH)
+    g = engine_mod.run(spec)
+    c = oracle_mod.run(spec, mode="philox")
+    for f in g.summaries.dtype.names:
+        np.testing.assert_array_equal(g.summaries[f], c.summaries[f], err_msg=f)
+    np.testing.assert_array_equal(g.hist, c.hist)
+
+
+@pytest.mark.gpu
+def test_engine_reproduces_parity_fixture(engine_mod):
+    """The GPU reproduces the committed oracle fixtures without running the oracle."""
+    import make_golden
+    from cases import cases
+
+    fx = np.load(os.path.join(GOLDEN, "parity_cases.npz"))
+    for name, spec in sorted(cases().items()):
+        r = engine_mod.run(spec, want_rows=True)
+        want = fx[f"{name}__summaries"]
+        for f in want.dtype.names:
+            np.testing.assert_array_equal(r.summaries[f], want[f], err_msg=f"{name}: {f}")
+        np.testing.assert_array_equal(r.hist, fx[f"{name}__hist"], err_msg=name)
+        assert make_golden.rows_digest(r) == str(fx[f"{name}__rows_sha256"]), name
+
+
+@pytest.mark.gpu
+def test_abc_sweep_shape_small(engine_mod, oracle_mod):
+    """C4 shape scaled down: 64 parameter sets x 32 replicates, per-set rates; every set's histogram
+    matches the oracle, and each set's totals count its own replicates only."""
+    rates, inits = [], []
+    for i in range(64):
+        s = 1.0 + 1.5 * (i % 16) / 15
+        d = 0.7 * (i // 16) / 3
+        rates.append((1.0, s, d, d))
+        inits.append({1 << (i % 4): 1})
+    spec = abi.RunSpec(seed=42, process=abi.BIRTH_DEATH, rates=rates, reps_per_set=32, n_replicates=64 * 32,
+                       max_cells=1000, hist_bins=513, init_per_set=inits, flags=abi.FLAG_EVENT_HASH)
+    g = engine_mod.run(spec)
+    c = oracle_mod.run(spec)
+    np.testing.assert_array_equal(g.hist, c.hist)
+    np.testing.assert_array_equal(g.summaries["event_hash"], c.summaries["event_hash"])
+    assert np.all(g.totals["replicates"] == 32)

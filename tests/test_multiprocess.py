@@ -1,0 +1,77 @@
+"""Multi-process sharding on CPU (gloo, world_size 2): the N>1 path of bench.py restated with the
+oracle as the per-rank engine. Each rank runs its contiguous global-id shard; one all-reduce sums
+histograms and totals; the result must be bit-identical to a single-process run of all replicates
+(the 1-GPU == N-GPU identity)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from ecdna_evo_amd import abi, shard
+
+
+def _spec(first, n, total):
+    return abi.RunSpec(seed=42, process=abi.BIRTH_DEATH, segregation=abi.SEG_BINOMIAL,
+                       rates=((1.0, 1.0, 0.1, 0.1), (1.0, 1.5, 0.3, 0.3), (1.0, 2.0, 0.5, 0.2)),
+                       reps_per_set=total // 3, first_replicate=first, n_replicates=n, max_cells=500,
+                       hist_bins=129, flags=abi.FLAG_EVENT_HASH)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, total, port, outdir, mode):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.join(os.path.dirname(here), "ecdna-evo_amd"), os.path.join(os.path.dirname(here), "oracle")]
+    import oracle
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if mode == "strong":
+        first, n = shard.shard_range(rank, world, total)
+    else:
+        first, n = shard.weak_range(rank, total // world)
+    r = oracle.run(_spec(first, n, total), mode="philox", n_threads=2)
+    hist = torch.from_numpy(r.hist.astype(np.int64).reshape(-1).copy())
+    tot = torch.from_numpy(r.totals.view(np.uint64).astype(np.int64).reshape(-1).copy())
+    shard.reduce_outputs(hist, tot)
+    np.save(os.path.join(outdir, f"summ{rank}.npy"), r.summaries)
+    if rank == 0:
+        np.save(os.path.join(outdir, "hist.npy"), hist.numpy())
+        np.save(os.path.join(outdir, "tot.npy"), tot.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["strong", "weak"])
+def test_two_rank_shards_reduce_to_single_run(oracle_mod, tmp_path, mode):
+    world, total = 2, 600
+    mp.spawn(_worker, args=(world, total, _free_port(), str(tmp_path), mode), nprocs=world, join=True)
+    full = oracle_mod.run(_spec(0, total, total), mode="philox")
+    np.testing.assert_array_equal(np.load(tmp_path / "hist.npy"), full.hist.astype(np.int64).reshape(-1))
+    np.testing.assert_array_equal(np.load(tmp_path / "tot.npy"), full.totals.view(np.uint64).astype(np.int64).reshape(-1))
+    summ = np.concatenate([np.load(tmp_path / f"summ{r}.npy") for r in range(world)])
+    for f in full.summaries.dtype.names:
+        np.testing.assert_array_equal(summ[f], full.summaries[f])
+
+
+def test_shard_ranges_partition():
+    for total in (1, 7, 1000, 2**20):
+        for world in (1, 2, 3, 8):
+            rs = [shard.shard_range(r, world, total) for r in range(world)]
+            assert rs[0][0] == 0
+            for (f0, n0), (f1, _) in zip(rs, rs[1:]):
+                assert f0 + n0 == f1
+            assert sum(n for _, n in rs) == total
