@@ -99,6 +99,7 @@ struct ecdna_ssa_ctx {
     uint64_t row_stride = 0;
     uint64_t chunk_reps = 0;
     uint32_t stepper_blocks_cap = 0;
+    int window = 1;  // LDS tail window stepper (ECDNA_SSA_WINDOW=0 selects the HBM-only variant)
     // owned copies of the host inputs
     std::vector<ecdna_rates_t> rates;
     std::vector<uint16_t> init_copies;
@@ -288,9 +289,10 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
     }
 
     // persistent stepper grid: as many resident lanes as the occupancy allows
+    c->window = env_u64("ECDNA_SSA_WINDOW", 1) ? 1 : 0;
     int per_cu = 0;
-    CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ecdna::stepper_kernel(p->process, p->segregation),
-                                                         ecdna::kStepperBlock, 0));
+    CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, ecdna::stepper_kernel(p->process, p->segregation, c->window), ecdna::kStepperBlock, 0));
     uint64_t bpc = env_u64("ECDNA_SSA_BLOCKS_PER_CU", 0);
     if (bpc) per_cu = (int)bpc;
     if (per_cu < 1) per_cu = 1;
@@ -348,7 +350,7 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
         const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(need, c->stepper_blocks_cap));
 
         HIP_TRY(hipEventRecord(ch.ev[0], st));
-        HIP_TRY(ecdna::launch_stepper(a, p.process, p.segregation, blocks, st));
+        HIP_TRY(ecdna::launch_stepper(a, p.process, p.segregation, c->window, blocks, st));
         HIP_TRY(hipEventRecord(ch.ev[1], st));
 
         ecdna::HistArgs hsa{};

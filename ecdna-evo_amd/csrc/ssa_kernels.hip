@@ -30,8 +30,25 @@ constexpr uint64_t kFnvOffset = 0xcbf29ce484222325ull;
 constexpr uint64_t kFnvPrime = 0x100000001b3ull;
 constexpr uint32_t kNoUnevenMaxTries = 4096;
 
-template <bool BD, int SEG>
+// LDS tail window (WIN): the last cells of each lane's row — the stack end that swap_remove reads
+// and the daughter pushes write — live in LDS, cells [wb, np); cells [0, wb) live in HBM. Ring
+// slot = position % kWin, laid out [slot][lane] so a wave's 2-B accesses spread over the banks.
+// The window is flushed / refilled in aligned 16-cell (32-B, one HBM write sector) blocks, so the
+// pushes cost ~1/16 of a write request instead of one each. Invariant: 1 <= np - wb <= kWin
+// whenever np > 0; wb is a multiple of kFlush.
+// Explicitly global (address space 1) 2-B load: pointers read from the kernel-argument struct are
+// generic, and the optimizer would otherwise fuse the LDS and HBM reads of cell_get into a flat load.
+__device__ __forceinline__ uint32_t gload_u16(const uint16_t* p) {
+    return *(const __attribute__((address_space(1))) uint16_t*)p;
+}
+
+constexpr uint32_t kWin = 32;
+constexpr uint32_t kFlush = 16;
+
+template <bool BD, int SEG, bool WIN>
 __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a) {
+    __shared__ uint16_t win[WIN ? kWin + 1 : 1][kStepperBlock];  // + 1 spare row
+    const uint32_t tid = threadIdx.x;
     const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
     const bool f32t = (a.flags & ECDNA_FLAG_TIME_F32) != 0;
     const bool hash_on = (a.flags & ECDNA_FLAG_EVENT_HASH) != 0;
@@ -39,9 +56,49 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
     bool active = false, have = false;
     uint32_t li = 0;
     uint64_t rid = 0;
-    uint16_t* row = nullptr;
-    uint32_t nm = 0, np = 0, tail = 0;
+    uint16_t* row = a.rows;  // (not nullptr: keeps the pointer provably global, no flat_* accesses)
+    uint32_t nm = 0, np = 0, tail = 0, wb = 0;
     bool tail_ok = false;
+
+    // cell access through the window (WIN) or straight to HBM
+    auto slot = [&](uint32_t pos) -> uint16_t& { return win[WIN ? (pos & (kWin - 1)) : 0][tid]; };
+    // LDS side unconditional (a spare row absorbs stores outside the window), HBM side under the
+    // branch: symmetric conditional accesses would be merged into one flat_load / flat_store.
+    auto cell_get = [&](uint32_t pos) -> uint32_t {
+        if (!WIN) return row[pos];
+        uint32_t v = slot(pos);
+        if (pos < wb) v = gload_u16(row + pos);
+        return v;
+    };
+    auto cell_put = [&](uint32_t pos, uint32_t v) {
+        if (!WIN) {
+            row[pos] = (uint16_t)v;
+            return;
+        }
+        const bool in_win = pos >= wb;
+        win[in_win ? (pos & (kWin - 1)) : kWin][tid] = (uint16_t)v;
+        if (!in_win) row[pos] = (uint16_t)v;
+    };
+    auto flush_block = [&]() {  // cells [wb, wb + 16) -> HBM as two 16-B stores; wb += 16
+        uint32_t p[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) p[j] = (uint32_t)slot(wb + 2 * j) | ((uint32_t)slot(wb + 2 * j + 1) << 16);
+        uint4* dst = reinterpret_cast<uint4*>(row + wb);
+        dst[0] = make_uint4(p[0], p[1], p[2], p[3]);
+        dst[1] = make_uint4(p[4], p[5], p[6], p[7]);
+        wb += kFlush;
+    };
+    auto refill_block = [&]() {  // wb -= 16; cells [wb, wb + 16) HBM -> LDS
+        wb -= kFlush;
+        const uint4* src = reinterpret_cast<const uint4*>(row + wb);
+        const uint4 x0 = src[0], x1 = src[1];
+        const uint32_t p[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            slot(wb + 2 * j) = (uint16_t)(p[j] & 0xffffu);
+            slot(wb + 2 * j + 1) = (uint16_t)(p[j] >> 16);
+        }
+    };
     float b0 = 0.f, b1 = 0.f, d0 = 0.f, d1 = 0.f;
     double t = 0.0;
     float t32 = 0.f;
@@ -52,6 +109,8 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
     for (;;) {
         if (!active) {
             if (have) {
+                if (WIN)
+                    for (uint32_t j = wb; j < np; ++j) row[j] = slot(j);  // whole row back in HBM
                 ecdna_rep_summary_t* s = a.summaries + li;
                 s->nminus = nm;
                 s->nplus = np;
@@ -85,7 +144,13 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
                 src = a.init_copies + a.init_offsets[set];
                 cnt = a.init_offsets[set + 1] - a.init_offsets[set];
             }
-            for (uint32_t j = 0; j < cnt; ++j) row[j] = src[j];
+            wb = (WIN && cnt) ? ((cnt - 1) / kFlush) * kFlush : 0;
+            if (WIN) {
+                for (uint32_t j = 0; j < wb; ++j) row[j] = src[j];
+                for (uint32_t j = wb; j < cnt; ++j) slot(j) = src[j];
+            } else {
+                for (uint32_t j = 0; j < cnt; ++j) row[j] = src[j];
+            }
             np = cnt;
             nm = (uint32_t)(a.init_nminus_set ? a.init_nminus_set[set] : a.init_nminus);
             tail_ok = false;
@@ -136,7 +201,7 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
         }
 
         if (!tail_ok && np > 0) {  // refill the cached tail value (after a DeathNPlus)
-            tail = row[np - 1];
+            tail = cell_get(np - 1);
             tail_ok = true;
         }
 
@@ -174,7 +239,7 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
                 }
             }
             idx = (uint32_t)(m >> 32);
-            if (ch == 1u) k = (idx == np - 1) ? tail : (uint32_t)row[idx];
+            if (ch == 1u) k = (idx == np - 1) ? tail : cell_get(idx);
         }
 
         // waiting time: independent of the load above, hides its latency
@@ -227,14 +292,15 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
                 active = false;
                 continue;
             }
-            if (idx != np - 1) row[idx] = (uint16_t)tail;  // swap_remove(idx)
+            if (idx != np - 1) cell_put(idx, tail);  // swap_remove(idx)
             if (un == 0u) {
-                row[np - 1] = (uint16_t)k1v;  // push k1, push k2
-                row[np] = (uint16_t)(n - k1v);
+                cell_put(np - 1, k1v);  // push k1, push k2
+                if (WIN && np - wb == kWin) flush_block();
+                cell_put(np, n - k1v);
                 np += 1;
                 tail = n - k1v;
             } else {
-                row[np - 1] = (uint16_t)n;  // push k1 + k2
+                cell_put(np - 1, n);  // push k1 + k2
                 tail = n;
                 if (un == 1u) nm += 1;
                 n_un += 1;
@@ -242,9 +308,14 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
             x |= ((uint64_t)k1v << 2) | ((uint64_t)idx << 20);
             n_pp += 1;
         } else if (BD && ch == 3u) {  // CellDeath::decrease_nplus (src/proliferation.rs:126-133)
-            if (idx != np - 1) row[idx] = (uint16_t)tail;
+            if (idx != np - 1) cell_put(idx, tail);
             np -= 1;
-            tail_ok = (np > 0) && (idx == np - 1);
+            if (WIN) {
+                if (np > 0 && np == wb) refill_block();  // keep the window non-empty
+                tail_ok = false;  // re-read from LDS at the next event
+            } else {
+                tail_ok = (np > 0) && (idx == np - 1);
+            }
             x |= (uint64_t)idx << 20;
             n_dp += 1;
         } else if (ch == 0u) {  // increase_nminus (src/proliferation.rs:113-117)
@@ -325,22 +396,24 @@ __global__ void __launch_bounds__(kHistBlock) ssa_hist(const HistArgs a) {
 
 // ---------------------------------------------------------------- launch
 
-#define ECDNA_STEPPER_TABLE(BD) \
-    {(const void*)ssa_stepper<BD, 0>, (const void*)ssa_stepper<BD, 1>, (const void*)ssa_stepper<BD, 2>, \
-     (const void*)ssa_stepper<BD, 3>}
+#define ECDNA_STEPPER_TABLE(BD, WIN)                                                                        \
+    {(const void*)ssa_stepper<BD, 0, WIN>, (const void*)ssa_stepper<BD, 1, WIN>,                             \
+     (const void*)ssa_stepper<BD, 2, WIN>, (const void*)ssa_stepper<BD, 3, WIN>}
 
-static const void* const kStepperTable[2][4] = {ECDNA_STEPPER_TABLE(false), ECDNA_STEPPER_TABLE(true)};
+static const void* const kStepperTable[2][2][4] = {
+    {ECDNA_STEPPER_TABLE(false, false), ECDNA_STEPPER_TABLE(true, false)},
+    {ECDNA_STEPPER_TABLE(false, true), ECDNA_STEPPER_TABLE(true, true)}};
 
-const void* stepper_kernel(int birth_death, int segregation) {
-    return kStepperTable[birth_death ? 1 : 0][segregation & 3];
+const void* stepper_kernel(int birth_death, int segregation, int window) {
+    return kStepperTable[window ? 1 : 0][birth_death ? 1 : 0][segregation & 3];
 }
 
-hipError_t launch_stepper(const StepperArgs& a, int birth_death, int segregation, uint32_t blocks,
+hipError_t launch_stepper(const StepperArgs& a, int birth_death, int segregation, int window, uint32_t blocks,
                           hipStream_t stream) {
     StepperArgs copy = a;
     void* args[] = {&copy};
-    return hipLaunchKernel(stepper_kernel(birth_death, segregation), dim3(blocks), dim3(kStepperBlock), args, 0,
-                           stream);
+    return hipLaunchKernel(stepper_kernel(birth_death, segregation, window), dim3(blocks), dim3(kStepperBlock), args,
+                           0, stream);
 }
 
 hipError_t launch_hist(const HistArgs& a, uint32_t blocks, hipStream_t stream) {

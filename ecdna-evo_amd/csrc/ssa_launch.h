@@ -53,8 +53,9 @@ constexpr int kHistBlock = 256;
 constexpr uint32_t kMaxHistBins = 4096;  // LDS: 8 B per bin per workgroup (<= 64 KiB)
 
 // Kernel handle for occupancy queries and the launch itself.
-const void* stepper_kernel(int birth_death, int segregation);
-hipError_t launch_stepper(const StepperArgs& a, int birth_death, int segregation, uint32_t blocks,
+// window: 1 = LDS tail window variant (default), 0 = rows straight in HBM (A/B reference)
+const void* stepper_kernel(int birth_death, int segregation, int window);
+hipError_t launch_stepper(const StepperArgs& a, int birth_death, int segregation, int window, uint32_t blocks,
                           hipStream_t stream);
 hipError_t launch_hist(const HistArgs& a, uint32_t blocks, hipStream_t stream);
 

@@ -31,6 +31,11 @@ def cases():
     # turnover: d close to b, 1000 initial cells, time-capped (C5 shape, scaled down)
     c["bd_turnover"] = abi.RunSpec(seed=13, process=abi.BIRTH_DEATH, rates=((1.0, 1.0, 0.9, 0.9),),
                                    n_replicates=16, max_cells=1_300, max_time=3.0, init={1: 1000}, flags=H)
+    # shrinking populations: N+ deaths walk the LDS tail window down through many 16-cell blocks
+    c["bd_shrink"] = abi.RunSpec(seed=19, process=abi.BIRTH_DEATH, rates=((1.0, 0.6, 0.2, 1.4),), n_replicates=32,
+                                 max_cells=5000, init={1: 150, 2: 60, 9: 37}, flags=H)
+    c["bd_oscillate"] = abi.RunSpec(seed=23, process=abi.BIRTH_DEATH, rates=((0.5, 1.0, 0.5, 1.0),),
+                                    n_replicates=32, max_cells=100, max_time=40.0, init={3: 33}, flags=H)
     # extinction-prone: death > birth -> Absorbing
     c["bd_extinction"] = abi.RunSpec(seed=17, process=abi.BIRTH_DEATH, rates=((1.0, 1.0, 1.5, 1.5),),
                                      n_replicates=64, max_cells=400, init={2: 3}, flags=H)

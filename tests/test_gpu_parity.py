@@ -73,3 +73,12 @@ def test_gpu_grid_size_does_not_change_results(engine_mod, monkeypatch):
     b = engine_mod.run(spec)
     np.testing.assert_array_equal(a.summaries["event_hash"], b.summaries["event_hash"])
     np.testing.assert_array_equal(a.hist, b.hist)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["pb_binomial_c1", "bd_binomial", "bd_shrink", "bd_turnover", "big_copies", "abc_sets"])
+def test_gpu_hbm_only_variant_matches_oracle(name, engine_mod, oracle_mod, monkeypatch):
+    """The A/B reference variant without the LDS tail window (ECDNA_SSA_WINDOW=0) is exact too."""
+    monkeypatch.setenv("ECDNA_SSA_WINDOW", "0")
+    spec = CASES[name]
+    _compare(engine_mod.run(spec, want_rows=True), oracle_mod.run(spec, mode="philox", want_rows=True), name)
