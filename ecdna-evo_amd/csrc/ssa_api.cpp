@@ -293,6 +293,10 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
     int per_cu = 0;
     CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &per_cu, ecdna::stepper_kernel(p->process, p->segregation, c->window), ecdna::kStepperBlock, 0));
+    // Memory-level parallelism of the random row accesses saturates HBM at about 3 resident 256-lane
+    // blocks per CU (C3 sweep, DESIGN.md §8: 1/2/3/4/7 blocks -> 617/372/329/336/349 ms); fewer
+    // lanes also mean more replicates per lane and a shorter drain once the work queue is empty.
+    per_cu = std::min(per_cu, 3);
     uint64_t bpc = env_u64("ECDNA_SSA_BLOCKS_PER_CU", 0);
     if (bpc) per_cu = (int)bpc;
     if (per_cu < 1) per_cu = 1;

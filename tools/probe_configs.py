@@ -1,0 +1,67 @@
+"""Throughput of the engine on every BASELINE.json config shape that runs on one GPU
+(configs[1..4]; C4 and C5 as the per-GPU shard of their 8-GPU runs). Development/measurement tool.
+Usage: python tools/probe_configs.py [c2 c3 c4 c5]"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ecdna-evo_amd"))
+from ecdna_evo_amd import abi, engine  # noqa: E402
+
+
+def c4_shard(rank=0, gpus=8):
+    """ABC sweep: 1024 (b1, d, k0) sets x 4096 replicates; rank 0's 128 sets."""
+    rates, inits = [], []
+    for i in range(1024):
+        s = 1.0 + 1.5 * (i % 16) / 15.0
+        d = 0.7 * ((i // 16) % 8) / 7.0
+        k0 = 1 << (i // 128)
+        rates.append((1.0, s, d, d))
+        inits.append({k0: 1})
+    per = 4096
+    n = 1024 * per // gpus
+    return abi.RunSpec(seed=42, process=abi.BIRTH_DEATH, rates=rates, reps_per_set=per, first_replicate=rank * n,
+                       n_replicates=n, max_cells=10_000, init_per_set=inits, hist_bins=1025, flags=0)
+
+
+def c5_shard(rank=0, gpus=8):
+    n = 262_144 // gpus
+    return abi.RunSpec(seed=42, process=abi.BIRTH_DEATH, rates=((1.0, 1.0, 0.9, 0.9),), reps_per_set=262_144,
+                       first_replicate=rank * n, n_replicates=n, max_cells=1_000_000, max_time=1000.0,
+                       init={1: 1000}, hist_bins=1025, flags=0)
+
+
+CONFIGS = {
+    "c2": lambda: abi.RunSpec(seed=42, n_replicates=65536, max_cells=10_000, flags=0),
+    "c3": lambda: abi.RunSpec(seed=42, process=abi.BIRTH_DEATH, rates=((1.0, 1.5, 0.3, 0.3),),
+                              n_replicates=1 << 20, max_cells=10_000, flags=0),
+    "c4": c4_shard,
+    "c5": c5_shard,
+}
+
+
+def main():
+    for name in sys.argv[1:] or list(CONFIGS):
+        spec = CONFIGS[name]()
+        t0 = time.time()
+        ctx = engine.Context(spec)
+        reps = 1 if name == "c5" else 2
+        for _ in range(reps):
+            t1 = time.time()
+            ctx.launch()
+            s_ms, h_ms = ctx.sync()
+            wall = time.time() - t1
+        res = ctx.download()
+        t = res.totals
+        ev = int(t["events"].sum())
+        print(json.dumps({"config": name, "replicates": spec.n_replicates, "events": ev, "stepper_ms": s_ms,
+                          "hist_ms": h_ms, "wall_ms": wall * 1e3, "events_per_s_kernel": ev / (s_ms * 1e-3),
+                          "events_per_s_wall": ev / wall, "geometry": ctx.geometry(),
+                          "stops": t["stop_reasons"].sum(axis=0).tolist(), "errors": int(t["errors"].sum()),
+                          "setup_s": t1 - t0}), flush=True)
+        ctx.close()
+
+
+if __name__ == "__main__":
+    main()
