@@ -71,6 +71,11 @@ int validate(const ecdna_ssa_params_t* p) {
     if (p->n_replicates && (p->first_replicate + p->n_replicates - 1) / p->reps_per_set >= p->n_param_sets)
         return fail(ECDNA_E_INVALID, "replicate ids map past the last parameter set");
     if (p->cell_cap == 0) return fail(ECDNA_E_INVALID, "cell_cap must be >= 1");
+    if (p->n_snapshots > ecdna::kMaxSnapshots) return fail(ECDNA_E_INVALID, "at most 64 snapshots");
+    if (p->n_snapshots && !p->snapshot_cells) return fail(ECDNA_E_INVALID, "snapshot_cells is NULL");
+    for (uint32_t q = 1; q < p->n_snapshots; ++q)
+        if (p->snapshot_cells[q] < p->snapshot_cells[q - 1])
+            return fail(ECDNA_E_INVALID, "snapshot_cells must be sorted ascending");
     if (!p->init_copies && (p->init_nplus || p->init_set_offsets))
         return fail(ECDNA_E_INVALID, "init_copies is NULL");
     for (uint32_t s = 0; s < p->n_param_sets; ++s) {
@@ -105,11 +110,15 @@ struct ecdna_ssa_ctx {
     std::vector<uint16_t> init_copies;
     std::vector<uint32_t> init_offsets;
     std::vector<uint64_t> init_nminus_set;
+    std::vector<uint64_t> snap_cells;
     // device buffers
     float4* d_rates = nullptr;
     uint16_t* d_init = nullptr;
     uint32_t* d_init_off = nullptr;
     uint64_t* d_init_nm = nullptr;
+    uint64_t* d_snap_cells = nullptr;
+    ecdna_snapshot_t* d_snap_meta = nullptr;
+    uint16_t* d_snap_rows = nullptr;
     uint16_t* d_rows = nullptr;
     ecdna_rep_summary_t* d_summ = nullptr;
     uint32_t* d_heads = nullptr;  // one work counter per chunk
@@ -152,6 +161,9 @@ void free_ctx(ecdna_ssa_ctx* c) {
     (void)hipFree(c->d_init);
     (void)hipFree(c->d_init_off);
     (void)hipFree(c->d_init_nm);
+    (void)hipFree(c->d_snap_cells);
+    (void)hipFree(c->d_snap_meta);
+    (void)hipFree(c->d_snap_rows);
     (void)hipFree(c->d_rows);
     (void)hipFree(c->d_summ);
     (void)hipFree(c->d_heads);
@@ -211,6 +223,8 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
     if (c->init_copies.empty()) c->init_copies.push_back(1);
     if (p->init_set_offsets) c->init_offsets.assign(p->init_set_offsets, p->init_set_offsets + p->n_param_sets + 1);
     if (p->init_set_nminus) c->init_nminus_set.assign(p->init_set_nminus, p->init_set_nminus + p->n_param_sets);
+    if (p->n_snapshots) c->snap_cells.assign(p->snapshot_cells, p->snapshot_cells + p->n_snapshots);
+    c->p.snapshot_cells = nullptr;
     c->p.rates = nullptr;
     c->p.init_copies = nullptr;
     c->p.init_set_offsets = nullptr;
@@ -252,6 +266,12 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
                           hipMemcpyHostToDevice));
     }
 
+    if (!c->snap_cells.empty()) {
+        CTX_TRY(hipMalloc(&c->d_snap_cells, c->snap_cells.size() * sizeof(uint64_t)));
+        CTX_TRY(hipMemcpy(c->d_snap_cells, c->snap_cells.data(), c->snap_cells.size() * sizeof(uint64_t),
+                          hipMemcpyHostToDevice));
+    }
+
     // outputs
     const uint64_t n = p->n_replicates;
     const uint64_t nb = (uint64_t)p->n_param_sets * p->hist_bins;
@@ -263,8 +283,14 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
     c->d_tot = c->d_tot_own;
     CTX_TRY(hipMalloc(&c->d_summ, std::max<uint64_t>(n, 1) * sizeof(ecdna_rep_summary_t)));
 
-    // rows: one u16 row per replicate of the chunk; chunk bounded by free HBM
     c->row_stride = round_up(p->cell_cap, 64);
+    if (p->n_snapshots && n) {  // snapshot outputs cover the whole run (not chunked)
+        CTX_TRY(hipMalloc(&c->d_snap_meta, n * p->n_snapshots * sizeof(ecdna_snapshot_t)));
+        if (p->flags & ECDNA_FLAG_SNAPSHOT_ROWS)
+            CTX_TRY(hipMalloc(&c->d_snap_rows, n * p->n_snapshots * c->row_stride * sizeof(uint16_t)));
+    }
+
+    // rows: one u16 row per replicate of the chunk; chunk bounded by free HBM
     const uint64_t row_bytes = c->row_stride * sizeof(uint16_t);
     size_t free_b = 0, total_b = 0;
     CTX_TRY(hipMemGetInfo(&free_b, &total_b));
@@ -325,6 +351,8 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
     HIP_TRY(hipMemsetAsync(c->d_tot, 0, p.n_param_sets * sizeof(ecdna_totals_t), st));
     if (!c->chunks.empty())
         HIP_TRY(hipMemsetAsync(c->d_heads, 0, c->chunks.size() * sizeof(uint32_t), st));
+    if (c->d_snap_meta)
+        HIP_TRY(hipMemsetAsync(c->d_snap_meta, 0, p.n_replicates * p.n_snapshots * sizeof(ecdna_snapshot_t), st));
 
     for (size_t k = 0; k < c->chunks.size(); ++k) {
         Chunk& ch = c->chunks[k];
@@ -350,6 +378,10 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
         a.cell_cap = p.cell_cap;
         a.flags = p.flags;
         a.cells_mul = (p.process == ECDNA_BIRTH_DEATH && (p.flags & ECDNA_FLAG_BD_CAP_COMPAT)) ? 2u : 1u;
+        a.n_snap = p.n_snapshots;
+        a.snap_cells = c->d_snap_cells;
+        a.snap_meta = c->d_snap_meta ? c->d_snap_meta + ch.first * p.n_snapshots : nullptr;
+        a.snap_rows = c->d_snap_rows ? c->d_snap_rows + ch.first * p.n_snapshots * c->row_stride : nullptr;
         const uint32_t need = (ch.n + ecdna::kStepperBlock - 1) / ecdna::kStepperBlock;
         const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(need, c->stepper_blocks_cap));
 
@@ -437,6 +469,22 @@ int ecdna_ssa_ctx_download(ecdna_ssa_ctx* c, ecdna_rep_summary_t* out_summaries,
         if (p.n_replicates)
             HIP_TRY(hipMemcpy(out_rows, c->d_rows, p.n_replicates * c->row_stride * sizeof(uint16_t),
                               hipMemcpyDeviceToHost));
+    }
+    return ECDNA_OK;
+}
+
+int ecdna_ssa_ctx_download_snapshots(ecdna_ssa_ctx* c, ecdna_snapshot_t* meta, uint16_t* rows) {
+    if (!c) return fail(ECDNA_E_INVALID, "ctx is NULL");
+    if (!c->launched) return fail(ECDNA_E_STATE, "download before launch");
+    const ecdna_ssa_params_t& p = c->p;
+    if (!p.n_snapshots || !p.n_replicates) return ECDNA_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->last_stream));
+    const uint64_t ns = p.n_replicates * p.n_snapshots;
+    if (meta) HIP_TRY(hipMemcpy(meta, c->d_snap_meta, ns * sizeof(ecdna_snapshot_t), hipMemcpyDeviceToHost));
+    if (rows) {
+        if (!c->d_snap_rows) return fail(ECDNA_E_STATE, "snapshot rows need ECDNA_FLAG_SNAPSHOT_ROWS");
+        HIP_TRY(hipMemcpy(rows, c->d_snap_rows, ns * c->row_stride * sizeof(uint16_t), hipMemcpyDeviceToHost));
     }
     return ECDNA_OK;
 }

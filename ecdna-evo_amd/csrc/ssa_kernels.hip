@@ -105,6 +105,7 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
     uint32_t e = 0, n_pm = 0, n_pp = 0, n_dm = 0, n_dp = 0, n_un = 0;
     uint64_t h = kFnvOffset;
     uint32_t stop = 0, err = 0;
+    uint32_t sj = 0;  // snapshots popped so far (the deque's front index)
 
     for (;;) {
         if (!active) {
@@ -160,6 +161,7 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
             h = kFnvOffset;
             stop = 0;
             err = 0;
+            sj = 0;
             if (np == 0 && nm == 0) {  // ensure!(!distribution.is_empty()) src/process.rs:88, 232
                 err = ECDNA_REP_ERR_EMPTY;
                 stop = ECDNA_STOP_ERROR;
@@ -197,6 +199,32 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
                 stop = s;
                 active = false;
                 continue;
+            }
+        }
+
+        // snapshots, checked at the top of advance_step before the event is applied
+        // (src/process.rs:122-145): while ANY remaining snapshot equals n- + n+, pop the FRONT one
+        // and save the current state into its slot.
+        if (a.n_snap) {
+            const uint64_t total = (uint64_t)nm + np;
+            while (sj < a.n_snap) {
+                bool any = false;
+                for (uint32_t q = 0; q < a.n_snap; ++q) any |= (q >= sj) && (a.snap_cells[q] == total);
+                if (!any) break;
+                ecdna_snapshot_t* m = a.snap_meta + (uint64_t)li * a.n_snap + sj;
+                m->time = f32t ? (double)t32 : t;
+                m->nminus = nm;
+                m->nplus = np;
+                m->taken = 1u;
+                m->reserved = 0u;
+                if (a.snap_rows) {
+                    uint16_t* dst = a.snap_rows + ((uint64_t)li * a.n_snap + sj) * a.row_stride;
+                    const uint32_t hbm_end = WIN ? (wb < np ? wb : np) : np;
+                    for (uint32_t j = 0; j < hbm_end; ++j) dst[j] = row[j];
+                    if (WIN)
+                        for (uint32_t j = hbm_end; j < np; ++j) dst[j] = slot(j);
+                }
+                ++sj;
             }
         }
 

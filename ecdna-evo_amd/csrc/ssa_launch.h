@@ -32,6 +32,10 @@ struct StepperArgs {
     uint32_t cell_cap;
     uint32_t flags;
     uint32_t cells_mul;             // 2 under ECDNA_FLAG_BD_CAP_COMPAT for birth-death, else 1
+    uint32_t n_snap;                // snapshots (0 = none)
+    const uint64_t* snap_cells;     // [n_snap], ascending
+    ecdna_snapshot_t* snap_meta;    // [n][n_snap], chunk-offset
+    uint16_t* snap_rows;            // [n][n_snap][row_stride] or nullptr, chunk-offset
 };
 
 // Histogram / totals pass over one chunk.
@@ -51,6 +55,7 @@ struct HistArgs {
 constexpr int kStepperBlock = 256;
 constexpr int kHistBlock = 256;
 constexpr uint32_t kMaxHistBins = 4096;  // LDS: 8 B per bin per workgroup (<= 64 KiB)
+constexpr uint32_t kMaxSnapshots = 64;
 
 // Kernel handle for occupancy queries and the launch itself.
 // window: 1 = LDS tail window variant (default), 0 = rows straight in HBM (A/B reference)

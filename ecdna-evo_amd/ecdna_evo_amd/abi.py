@@ -14,7 +14,7 @@ from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # ecdna_process_t (ProcessType, src/clap_app.rs:311-315)
 PURE_BIRTH = 0
@@ -45,6 +45,7 @@ REP_OK, REP_ERR_OVERFLOW, REP_ERR_EMPTY, REP_ERR_CELL_CAP, REP_ERR_REJECTION = r
 FLAG_TIME_F32 = 0x1
 FLAG_BD_CAP_COMPAT = 0x2
 FLAG_EVENT_HASH = 0x4
+FLAG_SNAPSHOT_ROWS = 0x8
 
 OK = 0
 E_INVALID, E_HIP, E_NOMEM, E_NODEVICE, E_STATE = -1, -2, -3, -4, -5
@@ -81,7 +82,25 @@ class Params(C.Structure):
         ("init_set_nminus", C.POINTER(C.c_uint64)),
         ("device", C.c_int32),
         ("reserved1", C.c_int32),
+        ("snapshot_cells", C.POINTER(C.c_uint64)),
+        ("n_snapshots", C.c_uint32),
+        ("reserved2", C.c_uint32),
     ]
+
+
+SNAPSHOT_DTYPE = np.dtype([("time", "<f8"), ("nminus", "<u8"), ("nplus", "<u8"), ("taken", "<u4"),
+                           ("reserved", "<u4")])
+assert SNAPSHOT_DTYPE.itemsize == 32
+
+
+def default_snapshots(cells: int, n_snapshots: int = 11):
+    """build_snapshots_from_cells (src/clap_app.rs:121-134): [1, 1+dx, ..., cells], dx = cells / 10."""
+    dx = cells // (n_snapshots - 1)
+    x = [1] * n_snapshots
+    for i in range(1, n_snapshots - 1):
+        x[i] = x[i - 1] + dx
+    x[n_snapshots - 1] = cells
+    return sorted(x)
 
 
 SUMMARY_DTYPE = np.dtype(
@@ -140,6 +159,7 @@ class RunSpec:
     init: Optional[Dict[int, int]] = None  # histogram {copies: cells}; default {1: 1} (src/clap_app.rs:188-191)
     init_per_set: Optional[List[Dict[int, int]]] = None
     device: int = 0
+    snapshots: Optional[Sequence[int]] = None  # cell counts (sorted here); None = no snapshots
     _keep: list = field(default_factory=list, repr=False)
 
     def resolved_max_time(self) -> float:
@@ -185,6 +205,11 @@ class RunSpec:
         p.max_iter = self.max_iter
         p.flags = self.flags
         p.device = self.device
+        if self.snapshots:
+            snaps = np.asarray(sorted(int(x) for x in self.snapshots), dtype=np.uint64)
+            self._keep.append(snaps)
+            p.snapshot_cells = _ptr(snaps, C.c_uint64)
+            p.n_snapshots = len(snaps)
         max_np = 0
         if self.init_per_set is not None:
             if len(self.init_per_set) != n_sets:

@@ -32,6 +32,7 @@ EXPORTS = [
     "ecdna_ssa_ctx_sync",
     "ecdna_ssa_ctx_device_outputs",
     "ecdna_ssa_ctx_download",
+    "ecdna_ssa_ctx_download_snapshots",
     "ecdna_ssa_ctx_row_stride",
     "ecdna_ssa_ctx_geometry",
     "ecdna_ssa_ctx_destroy",
@@ -84,6 +85,8 @@ def lib():
     L.ecdna_ssa_ctx_device_outputs.restype = C.c_int
     L.ecdna_ssa_ctx_download.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.ecdna_ssa_ctx_download.restype = C.c_int
+    L.ecdna_ssa_ctx_download_snapshots.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.ecdna_ssa_ctx_download_snapshots.restype = C.c_int
     L.ecdna_ssa_ctx_row_stride.argtypes = [C.c_void_p]
     L.ecdna_ssa_ctx_row_stride.restype = C.c_int64
     L.ecdna_ssa_ctx_geometry.argtypes = [C.c_void_p, P(C.c_uint64), P(C.c_uint64)]
@@ -114,9 +117,14 @@ class Result:
         self.totals = totals
         self.rows = rows
         self.row_stride = row_stride
+        self.snapshots = None  # [n][S] abi.SNAPSHOT_DTYPE
+        self.snapshot_rows = None  # [n][S][stride] u16 under FLAG_SNAPSHOT_ROWS
 
     def row(self, i: int) -> np.ndarray:
         return self.rows[i, : int(self.summaries[i]["nplus"])]
+
+    def snapshot_row(self, i: int, s: int) -> np.ndarray:
+        return self.snapshot_rows[i, s, : int(self.snapshots[i, s]["nplus"])]
 
 
 class Context:
@@ -176,7 +184,20 @@ class Context:
             rows = np.zeros((p.n_replicates, stride), dtype=np.uint16)
         _check(lib().ecdna_ssa_ctx_download(self.h, summ.ctypes.data, hist.ctypes.data, tot.ctypes.data,
                                             rows.ctypes.data if rows is not None else None), "download")
-        return Result(summ, hist.reshape(p.n_param_sets, p.hist_bins), tot, rows, stride)
+        res = Result(summ, hist.reshape(p.n_param_sets, p.hist_bins), tot, rows, stride)
+        if p.n_snapshots:
+            S = p.n_snapshots
+            meta = np.zeros((p.n_replicates, S), dtype=abi.SNAPSHOT_DTYPE)
+            srows = None
+            if p.flags & abi.FLAG_SNAPSHOT_ROWS:
+                st = (p.cell_cap + 63) // 64 * 64  # snapshot rows always use the 128-B aligned stride
+                srows = np.zeros((p.n_replicates, S, st), dtype=np.uint16)
+            _check(lib().ecdna_ssa_ctx_download_snapshots(self.h, meta.ctypes.data,
+                                                          srows.ctypes.data if srows is not None else None),
+                   "download_snapshots")
+            res.snapshots = meta
+            res.snapshot_rows = srows
+        return res
 
 
 def run(spec: "abi.RunSpec", want_rows: bool = False) -> Result:

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ECDNA_SSA_ABI_VERSION 1
+#define ECDNA_SSA_ABI_VERSION 2
 
 /* Process type — ProcessType (src/clap_app.rs:311-315); chosen as BirthDeath
  * when d0 > 0 or d1 > 0 (src/clap_app.rs:163-174, 194-200). */
@@ -95,6 +95,7 @@ typedef enum {
 #define ECDNA_FLAG_BD_CAP_COMPAT 0x2u  /* BD: stop at 2(n- + n+) >= max_cells, i.e. sum of the
                                           duplicated population vector (src/process.rs:339-344) */
 #define ECDNA_FLAG_EVENT_HASH 0x4u     /* fold every event into ecdna_rep_summary_t.event_hash */
+#define ECDNA_FLAG_SNAPSHOT_ROWS 0x8u  /* keep the N+ row of every snapshot (else only its metadata) */
 
 /* API return codes. */
 #define ECDNA_OK 0
@@ -141,7 +142,23 @@ typedef struct {
     const uint64_t* init_set_nminus;  /* host or NULL */
     int32_t device;                 /* HIP device ordinal for ecdna_ssa_run / ctx_create */
     int32_t reserved1;
+    /* Snapshots (--snapshots, src/clap_app.rs:92-97, 102-134; SavingOptions, src/lib.rs:21-25): cell
+     * counts, sorted ascending, at most 64. Before every event, while any REMAINING snapshot equals
+     * n- + n+, the FRONT one is popped and the current state saved (src/process.rs:122-145, the
+     * reference's pop_front-on-any-match rule). NULL / 0 = none. */
+    const uint64_t* snapshot_cells; /* host */
+    uint32_t n_snapshots;
+    uint32_t reserved2;
 } ecdna_ssa_params_t;
+
+/* One saved snapshot of one replicate (what process::save writes, src/process.rs:31-55). */
+typedef struct {
+    double time;                    /* process.time at the save (before the event's waiting time) */
+    uint64_t nminus;
+    uint64_t nplus;
+    uint32_t taken;                 /* 1 if this snapshot was popped (saved) during the run */
+    uint32_t reserved;
+} ecdna_snapshot_t;
 
 /* What run_simulations keeps of one replicate (src/main.rs:124-128, 198-210), plus counters. */
 typedef struct {
@@ -205,6 +222,10 @@ int ecdna_ssa_ctx_device_outputs(ecdna_ssa_ctx* c, uint64_t** d_hist, ecdna_tota
  * whole run fit in one chunk (ecdna_ssa_ctx_row_stride returns > 0). */
 int ecdna_ssa_ctx_download(ecdna_ssa_ctx* c, ecdna_rep_summary_t* out_summaries, uint64_t* out_hist,
                            ecdna_totals_t* out_totals, uint16_t* out_rows);
+/* Snapshots of the last launch: meta[n_replicates][n_snapshots] and, under ECDNA_FLAG_SNAPSHOT_ROWS,
+ * rows[n_replicates][n_snapshots][row_stride] u16 (the N+ cells in swap_remove order at the save).
+ * Either may be NULL. */
+int ecdna_ssa_ctx_download_snapshots(ecdna_ssa_ctx* c, ecdna_snapshot_t* meta, uint16_t* rows);
 /* Row stride (cells) of the rows buffer, or 0 when the run is chunked (rows not downloadable). */
 int64_t ecdna_ssa_ctx_row_stride(const ecdna_ssa_ctx* c);
 /* Replicates per chunk (memory bound) and lanes of the persistent stepper grid. */

@@ -55,6 +55,8 @@ def lib():
     L.oracle_increase_nplus.restype = C.c_int
     L.oracle_decrease_nplus.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32]
     L.oracle_decrease_nplus.restype = C.c_int
+    L.oracle_set_snapshot_outputs.argtypes = [C.c_void_p, C.c_void_p]
+    L.oracle_set_snapshot_outputs.restype = None
     L.oracle_increase_nminus.argtypes = [C.c_void_p]
     L.oracle_increase_nminus.restype = C.c_int
     L.oracle_decrease_nminus.argtypes = [C.c_void_p]
@@ -108,6 +110,9 @@ class OracleResult:
         n = int(self.summaries[i]["nplus"])
         return self.rows[i, :n]
 
+    def snapshot_row(self, i: int, s: int) -> np.ndarray:
+        return self.snapshot_rows[i, s, : int(self.snapshots[i, s]["nplus"])]
+
 
 def run(spec: "abi.RunSpec", mode: str = "philox", n_threads: int = 0, want_rows: bool = False) -> OracleResult:
     p = spec.params()
@@ -118,11 +123,21 @@ def run(spec: "abi.RunSpec", mode: str = "philox", n_threads: int = 0, want_rows
     stride = int(p.cell_cap)
     rows = np.zeros((n, stride), dtype=np.uint16) if want_rows else None
     fn = lib().oracle_run_philox if mode == "philox" else lib().oracle_run_compat
-    rc = fn(C.byref(p), summ.ctypes.data, hist.ctypes.data, tot.ctypes.data,
-            rows.ctypes.data if rows is not None else None, stride, n_threads)
+    S = p.n_snapshots
+    meta = np.zeros((n, S), dtype=abi.SNAPSHOT_DTYPE) if S else None
+    srows = np.zeros((n, S, p.cell_cap), dtype=np.uint16) if (S and p.flags & abi.FLAG_SNAPSHOT_ROWS) else None
+    lib().oracle_set_snapshot_outputs(meta.ctypes.data if meta is not None else None,
+                                      srows.ctypes.data if srows is not None else None)
+    try:
+        rc = fn(C.byref(p), summ.ctypes.data, hist.ctypes.data, tot.ctypes.data,
+                rows.ctypes.data if rows is not None else None, stride, n_threads)
+    finally:
+        lib().oracle_set_snapshot_outputs(None, None)
     if rc != 0:
         raise ValueError(f"oracle run failed: {rc}")
-    return OracleResult(summ, hist.reshape(p.n_param_sets, p.hist_bins), tot, rows, stride)
+    res = OracleResult(summ, hist.reshape(p.n_param_sets, p.hist_bins), tot, rows, stride)
+    res.snapshots, res.snapshot_rows = meta, srows
+    return res
 
 
 class Distr(C.Structure):

@@ -329,9 +329,15 @@ uint64_t oracle_compat_binomial(oracle_chacha* r, uint64_t n, double p) { return
 #define FNV_OFFSET 0xcbf29ce484222325ull
 #define FNV_PRIME 0x100000001b3ull
 
+void oracle_snapshot_check(const ecdna_ssa_params_t* p, uint32_t* sj, uint64_t nminus, uint64_t nplus,
+                           double time, const uint16_t* row, ecdna_snapshot_t* meta, uint16_t* rows,
+                           uint64_t stride);
+
 void oracle_compat_simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16_t* row,
-                                      ecdna_rep_summary_t* out) {
+                                      ecdna_rep_summary_t* out, ecdna_snapshot_t* snap_meta, uint16_t* snap_rows,
+                                      uint64_t snap_stride) {
     zig_init();
+    uint32_t sj = 0;
     const uint64_t set = rid / p->reps_per_set;
     const ecdna_rates_t rt = p->rates[set];
     const int bd = p->process == ECDNA_BIRTH_DEATH;
@@ -397,6 +403,8 @@ void oracle_compat_simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid,
             stop = ECDNA_STOP_ABSORBING;
             break;
         }
+        if (p->n_snapshots) /* advance_step's snapshot rule (src/process.rs:122-145) */
+            oracle_snapshot_check(p, &sj, nminus, nplus, (double)t, row, snap_meta, snap_rows, snap_stride);
         uint64_t x = (uint64_t)ch;
         if (ch == ECDNA_EV_PROLIF_NMINUS) {
             nminus += 1;

@@ -270,12 +270,46 @@ typedef struct {
     uint64_t* hist;
     ecdna_totals_t* totals;
     int compat;
+    ecdna_snapshot_t* snap_meta;
+    uint16_t* snap_rows;
 } run_ctx;
 
 #define FNV_OFFSET 0xcbf29ce484222325ull
 #define FNV_PRIME 0x100000001b3ull
 
 static inline uint64_t fnv_fold(uint64_t h, uint64_t x) { return (h ^ x) * FNV_PRIME; }
+
+static _Thread_local ecdna_snapshot_t* tl_snap_meta = NULL;
+static _Thread_local uint16_t* tl_snap_rows = NULL;
+
+void oracle_set_snapshot_outputs(ecdna_snapshot_t* meta, uint16_t* rows) {
+    tl_snap_meta = meta;
+    tl_snap_rows = rows;
+}
+
+/* The snapshot rule at the top of advance_step (src/process.rs:122-145, 267-290): while the deque is
+ * non-empty and ANY remaining snapshot equals n- + n+, pop the FRONT snapshot and save the current
+ * distribution (time before this event's waiting time). meta/rows: this replicate's [S] / [S][stride]
+ * outputs (either may be NULL). Shared with ssa_compat.c. */
+void oracle_snapshot_check(const ecdna_ssa_params_t* p, uint32_t* sj, uint64_t nminus, uint64_t nplus,
+                           double time, const uint16_t* row, ecdna_snapshot_t* meta, uint16_t* rows,
+                           uint64_t stride) {
+    const uint64_t total = nminus + nplus;
+    while (*sj < p->n_snapshots) {
+        int any = 0;
+        for (uint32_t q = *sj; q < p->n_snapshots; ++q) any |= p->snapshot_cells[q] == total;
+        if (!any) return;
+        if (meta) {
+            meta[*sj].time = time;
+            meta[*sj].nminus = nminus;
+            meta[*sj].nplus = nplus;
+            meta[*sj].taken = 1;
+            meta[*sj].reserved = 0;
+        }
+        if (rows) memcpy(rows + (uint64_t)*sj * stride, row, nplus * sizeof(uint16_t));
+        *sj += 1;
+    }
+}
 
 static void init_of_set(const ecdna_ssa_params_t* p, uint64_t set, const uint16_t** copies,
                         uint64_t* nplus, uint64_t* nminus) {
@@ -292,7 +326,9 @@ static void init_of_set(const ecdna_ssa_params_t* p, uint64_t set, const uint16_
 
 /* One replicate: the sosa::simulate loop around advance_step (SURVEY.md App. A.3 / DESIGN.md §3.1). */
 static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16_t* row,
-                               ecdna_rep_summary_t* out) {
+                               ecdna_rep_summary_t* out, ecdna_snapshot_t* snap_meta, uint16_t* snap_rows,
+                               uint64_t snap_stride) {
+    uint32_t sj = 0;
     const uint64_t set = rid / p->reps_per_set;
     const ecdna_rates_t rt = p->rates[set];
     const int bd = p->process == ECDNA_BIRTH_DEATH;
@@ -345,6 +381,9 @@ static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16
             stop = ECDNA_STOP_ABSORBING;
             break;
         }
+        if (p->n_snapshots)
+            oracle_snapshot_check(p, &sj, nminus, nplus, f32t ? (double)t32 : t, row, snap_meta, snap_rows,
+                                  snap_stride);
         uint32_t w[4];
         event_block(p->seed, rid, e, w);
         /* direct method: channel by w1 against the cumulative propensities */
@@ -401,7 +440,8 @@ static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16
 
 /* from ssa_compat.c */
 void oracle_compat_simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16_t* row,
-                                      ecdna_rep_summary_t* out);
+                                      ecdna_rep_summary_t* out, ecdna_snapshot_t* snap_meta, uint16_t* snap_rows,
+                                      uint64_t snap_stride);
 
 static void accumulate(const ecdna_ssa_params_t* p, uint64_t rid, const uint16_t* row,
                        const ecdna_rep_summary_t* s, uint64_t* hist, ecdna_totals_t* tot) {
@@ -437,10 +477,14 @@ static void* worker(void* arg) {
         uint64_t rid = p->first_replicate + i;
         uint16_t* row = c->rows ? c->rows + i * c->row_stride : scratch;
         ecdna_rep_summary_t s;
+        /* snapshot outputs: meta [n][S], rows [n][S][cell_cap] */
+        const uint64_t S = p->n_snapshots;
+        ecdna_snapshot_t* sm = c->snap_meta ? c->snap_meta + i * S : NULL;
+        uint16_t* sr = c->snap_rows ? c->snap_rows + i * S * p->cell_cap : NULL;
         if (c->compat)
-            oracle_compat_simulate_replicate(p, rid, row, &s);
+            oracle_compat_simulate_replicate(p, rid, row, &s, sm, sr, p->cell_cap);
         else
-            simulate_replicate(p, rid, row, &s);
+            simulate_replicate(p, rid, row, &s, sm, sr, p->cell_cap);
         if (c->summaries) c->summaries[i] = s;
         accumulate(p, rid, row, &s, hist, tot);
     }
@@ -487,6 +531,9 @@ static int validate(const ecdna_ssa_params_t* p, uint64_t row_stride, int want_r
     }
     if (maxn > p->cell_cap) return ECDNA_E_INVALID;
     if (want_rows && row_stride < p->cell_cap) return ECDNA_E_INVALID;
+    if (p->n_snapshots > 64 || (p->n_snapshots && !p->snapshot_cells)) return ECDNA_E_INVALID;
+    for (uint32_t q = 1; q < p->n_snapshots; ++q)
+        if (p->snapshot_cells[q] < p->snapshot_cells[q - 1]) return ECDNA_E_INVALID;
     return ECDNA_OK;
 }
 
@@ -507,6 +554,9 @@ static int run_pool(const ecdna_ssa_params_t* p, ecdna_rep_summary_t* out_summar
     c.hist = calloc(nb, sizeof(uint64_t));
     c.totals = calloc(p->n_param_sets, sizeof(ecdna_totals_t));
     c.compat = compat;
+    c.snap_meta = tl_snap_meta;
+    c.snap_rows = tl_snap_rows;
+    if (c.snap_meta) memset(c.snap_meta, 0, p->n_replicates * p->n_snapshots * sizeof(ecdna_snapshot_t));
     if (n_threads <= 0) n_threads = (int)sysconf(_SC_NPROCESSORS_ONLN);
     if (n_threads < 1) n_threads = 1;
     if ((uint64_t)n_threads > p->n_replicates) n_threads = p->n_replicates ? (int)p->n_replicates : 1;

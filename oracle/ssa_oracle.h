@@ -41,6 +41,9 @@ double oracle_softlog_neg(uint32_t w);
 int oracle_run_philox(const ecdna_ssa_params_t* p, ecdna_rep_summary_t* out_summaries,
                       uint64_t* out_hist, ecdna_totals_t* out_totals, uint16_t* out_rows,
                       uint64_t row_stride, int n_threads);
+/* Snapshot outputs for the next oracle_run_* call on this thread (NULL = discard):
+ * meta[n_replicates][n_snapshots], rows[n_replicates][n_snapshots][row_stride]. */
+void oracle_set_snapshot_outputs(ecdna_snapshot_t* meta, uint16_t* rows);
 /* Reference-semantics CPU path: stream of global replicate r is seed*10 + r (src/main.rs:56-58,
  * 213-215). Time is always accumulated in f32 like process.time (src/process.rs:184, 336);
  * ECDNA_FLAG_EVENT_HASH is honoured, ECDNA_FLAG_TIME_F32 is implied. */

@@ -64,4 +64,17 @@ def cases():
     c["nminus_only"] = abi.RunSpec(seed=6, n_replicates=4, max_cells=100, init={0: 5}, flags=H)
     c["already_full"] = abi.RunSpec(seed=6, n_replicates=4, max_cells=3, init={1: 3}, flags=H)
     c["no_hash"] = abi.RunSpec(seed=42, n_replicates=16, max_cells=500, flags=0)
+    # snapshots (src/process.rs:122-145): the reference's default 11 cell counts (clap_app.rs:121-134),
+    # the pop-front-on-any-match quirk (initial 50 cells, snapshots 1 and 40 popped with 51), and
+    # non-monotone birth-death totals
+    S = H | abi.FLAG_SNAPSHOT_ROWS
+    c["pb_snapshots_default"] = abi.RunSpec(seed=42, n_replicates=16, max_cells=1000,
+                                            snapshots=abi.default_snapshots(1000), flags=S)
+    c["pb_snapshots_quirk"] = abi.RunSpec(seed=8, n_replicates=16, max_cells=300, init={1: 50},
+                                          snapshots=[1, 40, 51, 60, 200, 300], flags=S)
+    c["bd_snapshots"] = abi.RunSpec(seed=29, process=abi.BIRTH_DEATH, rates=((1.0, 1.1, 0.9, 0.9),),
+                                    n_replicates=32, max_cells=400, init={2: 30}, snapshots=[20, 25, 31, 45, 90],
+                                    flags=S | abi.FLAG_TIME_F32)
+    c["bd_snapshots_meta_only"] = abi.RunSpec(seed=30, process=abi.BIRTH_DEATH, rates=BD_RATES, n_replicates=32,
+                                              max_cells=600, snapshots=abi.default_snapshots(600), flags=H)
     return c

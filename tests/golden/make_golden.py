@@ -38,6 +38,17 @@ def rows_digest(res) -> str:
     return h.hexdigest()
 
 
+def snapshot_digest(res) -> str:
+    h = hashlib.sha256()
+    if res.snapshot_rows is None:
+        return ""
+    for i in range(res.snapshots.shape[0]):
+        for s in range(res.snapshots.shape[1]):
+            h.update(res.snapshot_row(i, s).tobytes())
+            h.update(b"|")
+    return h.hexdigest()
+
+
 def c2_spec():
     return abi.RunSpec(seed=42, n_replicates=65536, max_cells=10_000, hist_bins=1025, flags=0)
 
@@ -49,6 +60,9 @@ def make_parity():
         out[f"{name}__summaries"] = r.summaries
         out[f"{name}__hist"] = r.hist
         out[f"{name}__rows_sha256"] = np.array(rows_digest(r))
+        if r.snapshots is not None:
+            out[f"{name}__snapshots"] = r.snapshots
+            out[f"{name}__snapshot_rows_sha256"] = np.array(snapshot_digest(r))
     np.savez_compressed(os.path.join(HERE, "parity_cases.npz"), **out)
 
 

@@ -25,6 +25,9 @@ def test_oracle_reproduces_parity_fixture(oracle_mod, parity, name):
         np.testing.assert_array_equal(r.summaries[f], want[f], err_msg=f"{name}: {f}")
     np.testing.assert_array_equal(r.hist, parity[f"{name}__hist"])
     assert make_golden.rows_digest(r) == str(parity[f"{name}__rows_sha256"])
+    if f"{name}__snapshots" in parity:
+        np.testing.assert_array_equal(r.snapshots, parity[f"{name}__snapshots"])
+        assert make_golden.snapshot_digest(r) == str(parity[f"{name}__snapshot_rows_sha256"])
 
 
 def test_oracle_reproduces_c2_compat_fixture(oracle_mod):

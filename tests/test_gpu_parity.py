@@ -24,6 +24,15 @@ def _compare(gpu, cpu, name):
     np.testing.assert_array_equal(gpu.hist, cpu.hist, err_msg=f"{name}: hist")
     for f in gpu.totals.dtype.names:
         np.testing.assert_array_equal(gpu.totals[f], cpu.totals[f], err_msg=f"{name}: totals.{f}")
+    if cpu.snapshots is not None:
+        for f in ("nminus", "nplus", "taken"):
+            np.testing.assert_array_equal(gpu.snapshots[f], cpu.snapshots[f], err_msg=f"{name}: snapshots.{f}")
+        np.testing.assert_array_equal(gpu.snapshots["time"].view(np.uint64), cpu.snapshots["time"].view(np.uint64))
+        if cpu.snapshot_rows is not None:
+            for i in range(len(gs)):
+                for s in range(cpu.snapshots.shape[1]):
+                    np.testing.assert_array_equal(gpu.snapshot_row(i, s), cpu.snapshot_row(i, s),
+                                                  err_msg=f"{name}: snapshot row {i}/{s}")
 
 
 @pytest.mark.gpu

@@ -112,6 +112,9 @@ def test_engine_reproduces_parity_fixture(engine_mod):
             np.testing.assert_array_equal(r.summaries[f], want[f], err_msg=f"{name}: {f}")
         np.testing.assert_array_equal(r.hist, fx[f"{name}__hist"], err_msg=name)
         assert make_golden.rows_digest(r) == str(fx[f"{name}__rows_sha256"]), name
+        if f"{name}__snapshots" in fx:
+            np.testing.assert_array_equal(r.snapshots, fx[f"{name}__snapshots"], err_msg=name)
+            assert make_golden.snapshot_digest(r) == str(fx[f"{name}__snapshot_rows_sha256"]), name
 
 
 @pytest.mark.gpu

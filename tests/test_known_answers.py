@@ -88,6 +88,31 @@ def test_segregation_law_chi2(oracle_mod, k):
     assert stats.chi2.sf(chi, keep.sum() - 1) > 1e-4
 
 
+@pytest.mark.parametrize("mode", MODES)
+def test_snapshot_rule_pops_front_on_any_match(oracle_mod, mode):
+    """src/process.rs:122-145: while ANY remaining snapshot equals n- + n+, pop the FRONT one and save.
+    From 50 initial cells with snapshots [1, 40, 51, ...], 1 and 40 are never reached but are popped
+    (and saved) together with 51; the last snapshot (= max_cells) is never saved by advance_step
+    because the run stops first."""
+    spec = abi.RunSpec(seed=8, n_replicates=32, max_cells=300, init={1: 50}, snapshots=[1, 40, 51, 60, 200, 300],
+                       flags=abi.FLAG_SNAPSHOT_ROWS)
+    r = oracle_mod.run(spec, mode=mode, want_rows=True)
+    m = r.snapshots
+    assert np.all(m["taken"][:, :5] == 1) and np.all(m["taken"][:, 5] == 0)
+    tot = m["nminus"] + m["nplus"]
+    assert np.all(tot[:, :3] == 51) and np.all(tot[:, 3] == 60) and np.all(tot[:, 4] == 200)
+    assert np.all(m["time"][:, 0] == m["time"][:, 2]) and np.all(m["time"][:, 2] < m["time"][:, 3])
+    for i in range(4):
+        assert np.array_equal(r.snapshot_row(i, 0), r.snapshot_row(i, 2))
+        assert len(r.snapshot_row(i, 4)) == m["nplus"][i, 4]
+
+
+def test_default_snapshots_match_clap_app():
+    """build_snapshots_from_cells(11, cells) (src/clap_app.rs:121-134)."""
+    assert abi.default_snapshots(1000) == [1, 101, 201, 301, 401, 501, 601, 701, 801, 901, 1000]
+    assert abi.default_snapshots(10) == [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 10]
+
+
 def _ks_pooled(h1, h2):
     c1, c2 = np.cumsum(h1) / h1.sum(), np.cumsum(h2) / h2.sum()
     return float(np.abs(c1 - c2).max())
