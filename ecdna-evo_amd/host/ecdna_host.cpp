@@ -1,0 +1,262 @@
+// ecdna_host.cpp — see ecdna_host.hpp.
+#include "ecdna_host.hpp"
+
+#include <sys/stat.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <charconv>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <set>
+#include <sstream>
+
+namespace ecdna {
+namespace host {
+
+std::map<uint32_t, uint64_t> Distribution::histogram() const {
+    std::map<uint32_t, uint64_t> h;
+    h[0] = nminus;
+    for (uint16_t k : nplus) h[k] += 1;
+    return h;
+}
+
+Distribution Distribution::from_histogram(const std::map<uint32_t, uint64_t>& h) {
+    Distribution d;
+    for (const auto& kv : h) {
+        if (kv.first == 0) {
+            d.nminus = kv.second;
+            continue;
+        }
+        if (kv.first > 65535) throw IoError("copy number " + std::to_string(kv.first) + " does not fit u16");
+        d.nplus.insert(d.nplus.end(), kv.second, (uint16_t)kv.first);
+    }
+    return d;
+}
+
+std::string to_json(const Distribution& d) {
+    std::string s = "{";
+    bool first = true;
+    for (const auto& kv : d.histogram()) {
+        if (!first) s += ",";
+        first = false;
+        s += "\"" + std::to_string(kv.first) + "\":" + std::to_string(kv.second);
+    }
+    return s + "}";
+}
+
+namespace {
+
+void skip_ws(const std::string& t, size_t& i) {
+    while (i < t.size() && (t[i] == ' ' || t[i] == '\n' || t[i] == '\r' || t[i] == '\t')) ++i;
+}
+
+uint64_t parse_uint(const std::string& t, size_t& i) {
+    size_t j = i;
+    while (j < t.size() && t[j] >= '0' && t[j] <= '9') ++j;
+    if (j == i) throw IoError("expected an unsigned integer at offset " + std::to_string(i));
+    uint64_t v = 0;
+    auto r = std::from_chars(t.data() + i, t.data() + j, v);
+    if (r.ec != std::errc()) throw IoError("integer out of range at offset " + std::to_string(i));
+    i = j;
+    return v;
+}
+
+}  // namespace
+
+Distribution from_json(const std::string& t) {
+    std::map<uint32_t, uint64_t> h;
+    size_t i = 0;
+    skip_ws(t, i);
+    if (i >= t.size() || t[i] != '{') throw IoError("expected '{'");
+    ++i;
+    skip_ws(t, i);
+    if (i < t.size() && t[i] == '}') return Distribution::from_histogram(h);
+    for (;;) {
+        skip_ws(t, i);
+        if (i >= t.size() || t[i] != '"') throw IoError("expected a quoted copy number");
+        ++i;
+        uint64_t k = parse_uint(t, i);
+        if (i >= t.size() || t[i] != '"') throw IoError("expected '\"'");
+        ++i;
+        skip_ws(t, i);
+        if (i >= t.size() || t[i] != ':') throw IoError("expected ':'");
+        ++i;
+        skip_ws(t, i);
+        uint64_t v = parse_uint(t, i);
+        if (k > 65535) throw IoError("copy number " + std::to_string(k) + " does not fit u16");
+        h[(uint32_t)k] += v;
+        skip_ws(t, i);
+        if (i < t.size() && t[i] == ',') {
+            ++i;
+            continue;
+        }
+        if (i < t.size() && t[i] == '}') break;
+        throw IoError("expected ',' or '}'");
+    }
+    return Distribution::from_histogram(h);
+}
+
+Distribution load_json(const std::string& path) {
+    std::ifstream f(path);
+    if (!f) throw IoError("cannot open " + path);
+    std::stringstream ss;
+    ss << f.rdbuf();
+    try {
+        return from_json(ss.str());
+    } catch (const IoError& e) {
+        throw IoError("cannot load the ecDNA distribution from " + path + ": " + e.what());
+    }
+}
+
+std::string rate_str(float r) {
+    char buf[64];
+    auto res = std::to_chars(buf, buf + sizeof(buf), r, std::chars_format::fixed);
+    std::string s(buf, res.ptr);
+    std::string out;
+    for (char c : s) {
+        if (c == '.')
+            out += "dot";
+        else
+            out += c;
+    }
+    return out;
+}
+
+std::string filename_pure_birth(float b0, float b1, uint64_t idx) {
+    return rate_str(b0) + "b0_" + rate_str(b1) + "b1_0d0_0d1_" + std::to_string(idx) + "idx";
+}
+
+std::string filename_birth_death(float b0, float b1, float d0, float d1, uint64_t idx) {
+    return rate_str(b0) + "b0_" + rate_str(b1) + "b1_" + rate_str(d0) + "d0_" + rate_str(d1) + "d1_" +
+           std::to_string(idx) + "idx";
+}
+
+std::string timepoint_dir(float time) {
+    char buf[64];
+    std::snprintf(buf, sizeof(buf), "%.1f", (double)time);
+    std::string out;
+    for (const char* p = buf; *p; ++p) {
+        if (*p == '.')
+            out += "dot";
+        else
+            out += *p;
+    }
+    return out + "years";
+}
+
+namespace {
+
+void mkdirs(const std::string& path) {
+    std::string cur;
+    for (size_t i = 0; i < path.size(); ++i) {
+        cur += path[i];
+        if ((path[i] == '/' && i > 0) || i + 1 == path.size()) {
+            if (::mkdir(cur.c_str(), 0755) != 0 && errno != EEXIST) throw IoError("cannot create dir " + cur);
+        }
+    }
+}
+
+}  // namespace
+
+std::string save(const std::string& dir, const std::string& filename, float time, const Distribution& d) {
+    std::string base = dir;
+    if (!base.empty() && base.back() != '/') base += '/';
+    const std::string folder = base + std::to_string(d.cells()) + "cells/ecdna/" + timepoint_dir(time);
+    mkdirs(folder);
+    const std::string path = folder + "/" + filename + ".json";
+    std::ofstream f(path);
+    if (!f) throw IoError("cannot write " + path);
+    f << to_json(d);
+    if (!f) throw IoError("cannot write " + path);
+    return path;
+}
+
+std::vector<uint64_t> default_snapshots(uint64_t cells, uint32_t n) {
+    const uint64_t dx = cells / (n - 1);
+    std::vector<uint64_t> x(n, 1);
+    for (uint32_t i = 1; i + 1 < n; ++i) x[i] = x[i - 1] + dx;
+    x[n - 1] = cells;
+    std::sort(x.begin(), x.end());
+    return x;
+}
+
+namespace {
+
+// Philox4x32-10 (Salmon et al. 2011) — the engine's generator, for host-side draws.
+void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+    for (int r = 0; r < 10; ++r) {
+        if (r) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n1 = (uint32_t)p1;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1, n3 = (uint32_t)p0;
+        c[0] = n0;
+        c[1] = n1;
+        c[2] = n2;
+        c[3] = n3;
+    }
+}
+
+struct Words {
+    uint32_t k0, k1, sample, rid_lo, rid_hi, block = 0, pos = 4;
+    uint32_t buf[4];
+    uint32_t next() {
+        if (pos == 4) {
+            buf[0] = sample;
+            buf[1] = 0x80000000u | block++;
+            buf[2] = rid_lo;
+            buf[3] = rid_hi;
+            philox(buf, k0, k1);
+            pos = 0;
+        }
+        return buf[pos++];
+    }
+    // uniform in [0, n), n in [1, 2^32): Lemire with exact rejection
+    uint32_t below(uint64_t n) {
+        uint64_t m = (uint64_t)next() * n;
+        uint32_t lo = (uint32_t)m;
+        if (lo < n) {
+            const uint32_t thr = (uint32_t)((0x100000000ull - n) % n);
+            while (lo < thr) {
+                m = (uint64_t)next() * n;
+                lo = (uint32_t)m;
+            }
+        }
+        return (uint32_t)(m >> 32);
+    }
+};
+
+}  // namespace
+
+Distribution subsample(const Distribution& d, uint64_t nb_cells, uint64_t seed, uint64_t rid, uint32_t sample_index) {
+    const uint64_t N = d.cells();
+    if (nb_cells >= N) return d;
+    if (N > 0xffffffffull) throw IoError("subsampling needs fewer than 2^32 cells");
+    Words w;
+    w.k0 = (uint32_t)seed;
+    w.k1 = (uint32_t)(seed >> 32);
+    w.sample = sample_index;
+    w.rid_lo = (uint32_t)rid;
+    w.rid_hi = (uint32_t)(rid >> 32);
+    std::set<uint64_t> pick;  // Floyd: for j in N-m .. N-1: t = U[0, j]; take t, or j if t was taken
+    for (uint64_t j = N - nb_cells; j < N; ++j) {
+        const uint64_t t = w.below(j + 1);
+        if (!pick.insert(t).second) pick.insert(j);
+    }
+    Distribution out;
+    for (uint64_t idx : pick) {
+        if (idx < d.nminus)
+            out.nminus += 1;
+        else
+            out.nplus.push_back(d.nplus[idx - d.nminus]);
+    }
+    return out;
+}
+
+}  // namespace host
+}  // namespace ecdna

@@ -1,0 +1,200 @@
+"""The native host around the hot path (CPU only): CLI option resolution mirroring Cli::build
+(src/clap_app.rs:137-229), output naming (src/lib.rs:27-45, src/process.rs:267-291), the JSON
+histogram format (dynamics.md:8) and end-of-run subsampling (src/main.rs:110-123)."""
+import ctypes as C
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(REPO, "ecdna-evo_amd", "bin", "ecdna-dynamics")
+HOSTLIB = os.path.join(REPO, "ecdna-evo_amd", "lib", "libecdna_host.so")
+
+
+@pytest.fixture(scope="module")
+def host():
+    if not (os.path.exists(CLI) and os.path.exists(HOSTLIB)):
+        import __graft_entry__
+
+        __graft_entry__.build()
+    L = C.CDLL(HOSTLIB)
+    L.ecdna_host_rate_str.argtypes = [C.c_float, C.c_char_p, C.c_size_t]
+    L.ecdna_host_timepoint_dir.argtypes = [C.c_float, C.c_char_p, C.c_size_t]
+    L.ecdna_host_filename.argtypes = [C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, C.c_uint64, C.c_char_p,
+                                      C.c_size_t]
+    L.ecdna_host_subsample.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
+                                       C.c_uint32, C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    L.ecdna_host_save.argtypes = [C.c_char_p, C.c_char_p, C.c_float, C.c_void_p, C.c_uint64, C.c_uint64, C.c_char_p,
+                                  C.c_size_t]
+    L.ecdna_host_load.argtypes = [C.c_char_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
+    L.ecdna_host_load.restype = C.c_int64
+    return L
+
+
+def _s(fn, *args):
+    buf = C.create_string_buffer(512)
+    assert fn(*args, buf, 512) >= 0
+    return buf.value.decode()
+
+
+def dry(*args):
+    out = subprocess.run([CLI, "--dry-run", *args, "/tmp/ecdna_out"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    return json.loads(out.stdout)
+
+
+def test_cli_defaults(host):
+    d = dry()
+    # clap defaults (src/clap_app.rs:35-99): seed 26, runs 12, cells 1000, years floor(log2(1000)+4) = 13
+    assert (d["process"], d["segregation"], d["seed"], d["runs"], d["cells"], d["years"]) == \
+        ("PureBirth", "binomial", 26, 12, 1000, 13)
+    assert d["snapshots"] == [1, 101, 201, 301, 401, 501, 601, 701, 801, 901, 1000]
+    assert d["initial"] == {"0": 0, "1": 1} and d["first_idx"] == 260 and d["parallel"] is True
+
+
+@pytest.mark.parametrize("cells,years", [(10, 7), (1000, 13), (10_000, 17), (1_000_000, 23), (3, 5)])
+def test_cli_years_from_cells(host, cells, years):
+    assert dry("--cells", str(cells))["years"] == years
+
+
+def test_cli_process_type_from_death_rates(host):
+    # is_birth_death = d0 > 0 | d1 > 0 (src/clap_app.rs:163-174)
+    assert dry("--d0", "0", "--d1", "0")["process"] == "PureBirth"
+    assert dry("--d1", "0.3")["process"] == "BirthDeath"
+    assert dry("--d0", "0.1")["process"] == "BirthDeath"
+
+
+def test_cli_years_mode_and_debug(host):
+    d = dry("--years", "20", "--runs", "3", "-s")
+    assert d["cells"] == 1_000_000_000 and d["years"] == 20 and d["runs"] == 3 and d["parallel"] is False
+    d = dry("-d")
+    assert (d["cells"], d["years"], d["runs"], d["verbosity"], d["parallel"]) == (300, 2, 1, 255, False)
+
+
+def test_cli_lists_and_segregation(host, tmp_path):
+    d = dry("--snapshots=50,5,500", "--subsamples=10,100", "--segregation", "binomial-no-uneven")
+    assert d["snapshots"] == [5, 50, 500] and d["subsamples"] == [10, 100]
+    assert d["segregation"] == "binomial-no-uneven"
+    init = tmp_path / "init.json"
+    init.write_text('{"0": 2, "1": 2, "10": 1, "20":1}')  # dynamics.md:8
+    assert dry("--initial", str(init))["initial"] == {"0": 2, "1": 2, "10": 1, "20": 1}
+
+
+@pytest.mark.parametrize("args", [["--cells", "5", "--years", "3"], ["-d", "--runs", "2"], ["--initial", "x.csv"],
+                                  ["--snapshots", "5"], ["--segregation", "nope"], ["--b0"], ["--bogus"]])
+def test_cli_rejects_like_clap(host, args):
+    out = subprocess.run([CLI, *args, "/tmp/x"], capture_output=True, text=True)
+    assert out.returncode == 2 and "error" in out.stderr
+
+
+def test_cli_without_device_fails_loudly(host, tmp_path):
+    from ecdna_evo_amd import engine
+
+    if engine.device_count() > 0:
+        pytest.skip("GPU present")
+    out = subprocess.run([CLI, str(tmp_path)], capture_output=True, text=True)
+    assert out.returncode == 1 and "gfx950" in out.stderr
+
+
+@pytest.mark.parametrize("x", [1.0, 1.5, 0.3, 0.1, 2.5e-5, 100.0, 0.9, 1.2, 3.3333333, 1e7])
+def test_rate_str_is_rust_f32_display(host, x):
+    want = np.format_float_positional(np.float32(x), trim="-").replace(".", "dot")
+    assert _s(host.ecdna_host_rate_str, x) == want
+
+
+@pytest.mark.parametrize("t,want", [(13.0, "13dot0years"), (0.25, "0dot2years"), (9.96, "10dot0years"),
+                                    (0.05, "0dot1years"), (5.75, "5dot8years"), (0.0, "0dot0years")])
+def test_timepoint_dir(host, t, want):
+    assert _s(host.ecdna_host_timepoint_dir, t) == want
+
+
+def test_filenames(host):
+    assert _s(host.ecdna_host_filename, 0, 1.0, 1.5, 0, 0, 420) == "1b0_1dot5b1_0d0_0d1_420idx"
+    assert _s(host.ecdna_host_filename, 1, 1.0, 1.5, 0.3, 0.3, 7) == "1b0_1dot5b1_0dot3d0_0dot3d1_7idx"
+
+
+def test_save_and_load_roundtrip(host, tmp_path):
+    cells = np.array([3, 1, 3, 20, 1, 1], np.uint16)
+    path = _s(host.ecdna_host_save, str(tmp_path).encode(), b"fname", 7.25, cells.ctypes.data, len(cells), 4)
+    assert path == f"{tmp_path}/10cells/ecdna/7dot2years/fname.json"
+    assert json.load(open(path)) == {"0": 4, "1": 3, "3": 2, "20": 1}
+    out = np.zeros(16, np.uint16)
+    nm = C.c_uint64()
+    n = host.ecdna_host_load(path.encode(), out.ctypes.data, 16, C.byref(nm))
+    assert n == 6 and nm.value == 4 and list(out[:n]) == [1, 1, 1, 3, 3, 20]
+
+
+def _philox(ctr, key):
+    M0, M1, W0, W1 = 0xD2511F53, 0xCD9E8D57, 0x9E3779B9, 0xBB67AE85
+    c = list(ctr)
+    k0, k1 = key
+    for r in range(10):
+        if r:
+            k0, k1 = (k0 + W0) & 0xFFFFFFFF, (k1 + W1) & 0xFFFFFFFF
+        p0, p1 = M0 * c[0], M1 * c[2]
+        c = [((p1 >> 32) ^ c[1] ^ k0) & 0xFFFFFFFF, p1 & 0xFFFFFFFF, ((p0 >> 32) ^ c[3] ^ k1) & 0xFFFFFFFF,
+             p0 & 0xFFFFFFFF]
+    return c
+
+
+def subsample_py(nplus, nminus, nb, seed, rid, k):
+    """Independent restatement of host::subsample (Floyd's algorithm over cell positions)."""
+    N = nminus + len(nplus)
+    if nb >= N:
+        return list(nplus), nminus
+    words, blk = [], 0
+
+    def nxt():
+        nonlocal blk
+        if not words:
+            words.extend(_philox([k, 0x80000000 | blk, rid & 0xFFFFFFFF, rid >> 32], [seed & 0xFFFFFFFF, seed >> 32]))
+            blk += 1
+        return words.pop(0)
+
+    def below(n):
+        m = nxt() * n
+        if (m & 0xFFFFFFFF) < n:
+            thr = (2**32 - n) % n
+            while (m & 0xFFFFFFFF) < thr:
+                m = nxt() * n
+        return m >> 32
+
+    pick = set()
+    for j in range(N - nb, N):
+        t = below(j + 1)
+        pick.add(j if t in pick else t)
+    out = [nplus[i - nminus] for i in sorted(pick) if i >= nminus]
+    return out, sum(1 for i in pick if i < nminus)
+
+
+@pytest.mark.parametrize("nb", [0, 1, 7, 50, 199, 200, 500])
+def test_subsample_matches_restatement(host, nb):
+    rng = np.random.default_rng(nb)
+    nplus = rng.integers(1, 60, 150).astype(np.uint16)
+    nminus = 50
+    out = np.zeros(200, np.uint16)
+    onp, onm = C.c_uint64(), C.c_uint64()
+    assert host.ecdna_host_subsample(nplus.ctypes.data, len(nplus), nminus, nb, 42, 421, 1, out.ctypes.data,
+                                     C.byref(onp), C.byref(onm)) == 0
+    want_p, want_m = subsample_py(nplus.tolist(), nminus, nb, 42, 421, 1)
+    assert list(out[: onp.value]) == want_p and onm.value == want_m
+    assert onp.value + onm.value == min(nb, 200)
+
+
+def test_subsample_is_uniform_without_replacement(host):
+    nplus = np.arange(1, 41, dtype=np.uint16)  # 40 distinct N+ cells, plus 10 N- cells
+    counts = np.zeros(41)
+    nm_total = 0
+    out = np.zeros(40, np.uint16)
+    onp, onm = C.c_uint64(), C.c_uint64()
+    for rid in range(3000):
+        host.ecdna_host_subsample(nplus.ctypes.data, 40, 10, 10, 7, rid, 0, out.ctypes.data, C.byref(onp), C.byref(onm))
+        sel = out[: onp.value]
+        assert len(set(sel.tolist())) == len(sel)  # without replacement
+        counts[sel] += 1
+        nm_total += onm.value
+    # each of the 50 cells is kept with probability 10/50
+    assert abs(counts[1:].mean() / 3000 - 0.2) < 0.01 and abs(nm_total / (3000 * 10) - 0.2) < 0.015
