@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -63,6 +64,8 @@ int validate(const ecdna_ssa_params_t* p) {
     if (p->reps_per_set == 0) return fail(ECDNA_E_INVALID, "reps_per_set must be >= 1");
     if (p->hist_bins < 2 || p->hist_bins > ecdna::kMaxHistBins)
         return fail(ECDNA_E_INVALID, "hist_bins must be in [2, 4096]");
+    if ((p->flags & ECDNA_FLAG_REP_STATS) && p->hist_bins > 2048)
+        return fail(ECDNA_E_INVALID, "ECDNA_FLAG_REP_STATS needs hist_bins <= 2048");
     if (p->process != ECDNA_PURE_BIRTH && p->process != ECDNA_BIRTH_DEATH)
         return fail(ECDNA_E_INVALID, "unknown process");
     if (p->segregation < 0 || p->segregation > 3) return fail(ECDNA_E_INVALID, "unknown segregation");
@@ -111,6 +114,11 @@ struct ecdna_ssa_ctx {
     std::vector<uint32_t> init_offsets;
     std::vector<uint64_t> init_nminus_set;
     std::vector<uint64_t> snap_cells;
+    // ABC statistics target
+    bool has_target = false;
+    double target_mean = 0.0, target_entropy = 0.0, target_freq = 0.0;
+    double* d_target_cdf = nullptr;
+    ecdna_rep_stats_t* d_stats = nullptr;
     // device buffers
     float4* d_rates = nullptr;
     uint16_t* d_init = nullptr;
@@ -164,6 +172,8 @@ void free_ctx(ecdna_ssa_ctx* c) {
     (void)hipFree(c->d_snap_cells);
     (void)hipFree(c->d_snap_meta);
     (void)hipFree(c->d_snap_rows);
+    (void)hipFree(c->d_target_cdf);
+    (void)hipFree(c->d_stats);
     (void)hipFree(c->d_rows);
     (void)hipFree(c->d_summ);
     (void)hipFree(c->d_heads);
@@ -271,6 +281,34 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
         CTX_TRY(hipMemcpy(c->d_snap_cells, c->snap_cells.data(), c->snap_cells.size() * sizeof(uint64_t),
                           hipMemcpyHostToDevice));
     }
+
+    // ABC statistics: the target's CDF over the bins and its mean / entropy / N+ frequency (the overflow bin
+    // counts at k = bins - 1), computed once on the host
+    if ((p->flags & ECDNA_FLAG_REP_STATS) && p->n_replicates) {
+        CTX_TRY(hipMalloc(&c->d_stats, p->n_replicates * sizeof(ecdna_rep_stats_t)));
+        if (p->stats_target_hist) {
+            const uint32_t bins = p->hist_bins;
+            double tot = 0.0;
+            for (uint32_t b = 0; b < bins; ++b) tot += (double)p->stats_target_hist[b];
+            if (!(tot > 0.0)) return bail(fail(ECDNA_E_INVALID, "stats_target_hist is empty"));
+            std::vector<double> cdf(bins);
+            double acc = 0.0, ksum = 0.0, ent = 0.0;
+            for (uint32_t b = 0; b < bins; ++b) {
+                const double pb = (double)p->stats_target_hist[b] / tot;
+                acc += pb;
+                cdf[b] = acc;
+                ksum += (double)b * (double)p->stats_target_hist[b];
+                if (pb > 0.0) ent -= pb * std::log(pb);
+            }
+            c->has_target = true;
+            c->target_mean = ksum / tot;
+            c->target_entropy = ent;
+            c->target_freq = 1.0 - (double)p->stats_target_hist[0] / tot;
+            CTX_TRY(hipMalloc(&c->d_target_cdf, bins * sizeof(double)));
+            CTX_TRY(hipMemcpy(c->d_target_cdf, cdf.data(), bins * sizeof(double), hipMemcpyHostToDevice));
+        }
+    }
+    c->p.stats_target_hist = nullptr;
 
     // outputs
     const uint64_t n = p->n_replicates;
@@ -403,6 +441,12 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
         uint32_t rpb = (ch.n + hist_blocks_max - 1) / hist_blocks_max;
         if (rpb < 4) rpb = 4;
         hsa.reps_per_block = rpb;
+        hsa.stats = c->d_stats ? c->d_stats + ch.first : nullptr;
+        hsa.target_cdf = c->d_target_cdf;
+        hsa.target_mean = c->target_mean;
+        hsa.target_entropy = c->target_entropy;
+        hsa.target_freq = c->target_freq;
+        hsa.has_target = c->has_target ? 1u : 0u;
         const uint32_t hblocks = (ch.n + rpb - 1) / rpb;
         HIP_TRY(ecdna::launch_hist(hsa, hblocks, st));
         HIP_TRY(hipEventRecord(ch.ev[2], st));
@@ -486,6 +530,17 @@ int ecdna_ssa_ctx_download_snapshots(ecdna_ssa_ctx* c, ecdna_snapshot_t* meta, u
         if (!c->d_snap_rows) return fail(ECDNA_E_STATE, "snapshot rows need ECDNA_FLAG_SNAPSHOT_ROWS");
         HIP_TRY(hipMemcpy(rows, c->d_snap_rows, ns * c->row_stride * sizeof(uint16_t), hipMemcpyDeviceToHost));
     }
+    return ECDNA_OK;
+}
+
+int ecdna_ssa_ctx_download_stats(ecdna_ssa_ctx* c, ecdna_rep_stats_t* out) {
+    if (!c) return fail(ECDNA_E_INVALID, "ctx is NULL");
+    if (!c->launched) return fail(ECDNA_E_STATE, "download before launch");
+    if (!c->d_stats) return fail(ECDNA_E_STATE, "statistics need ECDNA_FLAG_REP_STATS");
+    if (!out || !c->p.n_replicates) return ECDNA_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->last_stream));
+    HIP_TRY(hipMemcpy(out, c->d_stats, c->p.n_replicates * sizeof(ecdna_rep_stats_t), hipMemcpyDeviceToHost));
     return ECDNA_OK;
 }
 

@@ -362,15 +362,38 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
     }
 }
 
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS accesses have completed
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+
+__device__ __forceinline__ double wave_max(double x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = fmax(x, __shfl_xor(x, o, 64));
+    return x;
+}
+
 // Histogram + totals over one chunk. Each workgroup owns a contiguous range of replicates; per
 // parameter set it accumulates in LDS (u64 atomics) and flushes non-zero bins with one global
 // atomic each. Rows are read 16 B (8 cells) per lane per load.
+// STATS: each wave first builds its replicate's own histogram in LDS (u32 per bin), derives the
+// replicate's ABC statistics from it (mean, entropy, N+ frequency, KS distance to the target CDF by
+// a wave prefix scan over the bins — abc.md:38-55), then adds it to the workgroup histogram.
+template <bool STATS>
 __global__ void __launch_bounds__(kHistBlock) ssa_hist(const HistArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds[];
     unsigned long long* hb = lds;                // [bins]
     unsigned long long* tb = lds + a.bins;       // [16] totals words
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t nw = blockDim.x >> 6;
+    uint32_t* wh = reinterpret_cast<uint32_t*>(lds + a.bins + 16) + wave * a.bins;  // STATS: [bins] per wave
     const uint32_t r_begin = blockIdx.x * a.reps_per_block;
     if (r_begin >= a.n) return;
     const uint32_t r_end = min(a.n, r_begin + a.reps_per_block);
@@ -387,6 +410,11 @@ __global__ void __launch_bounds__(kHistBlock) ssa_hist(const HistArgs a) {
             const ecdna_rep_summary_t* s = a.summaries + q;
             const uint32_t np = (uint32_t)s->nplus;
             const uint16_t* row = a.rows + (uint64_t)q * a.row_stride;
+            if (STATS) {
+                for (uint32_t b = lane; b < a.bins; b += 64u) wh[b] = 0u;
+                wave_sync_lds();
+            }
+            uint64_t ksum = 0;
             for (uint32_t c = lane * 8u; c < np; c += 512u) {
                 const uint4 v = *reinterpret_cast<const uint4*>(row + c);
                 const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
@@ -394,12 +422,55 @@ __global__ void __launch_bounds__(kHistBlock) ssa_hist(const HistArgs a) {
                 for (int j = 0; j < 8; ++j) {
                     if (c + (uint32_t)j < np) {
                         const uint32_t kk = (wv[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
-                        atomicAdd(&hb[kk < last ? kk : last], 1ull);
+                        if (STATS) {
+                            atomicAdd(&wh[kk < last ? kk : last], 1u);
+                            ksum += kk;
+                        } else {
+                            atomicAdd(&hb[kk < last ? kk : last], 1ull);
+                        }
                     }
                 }
             }
+            if (STATS) {
+                if (lane == 0) atomicAdd(&wh[0], (uint32_t)s->nminus);
+                wave_sync_lds();
+                ksum = wave_sum(ksum);
+                const uint64_t cells = s->nminus + (uint64_t)np;
+                const double inv = cells ? 1.0 / (double)cells : 0.0;
+                double carry = 0.0, ent = 0.0, ks = 0.0;
+                for (uint32_t base = 0; base < a.bins; base += 64u) {
+                    const uint32_t b = base + lane;
+                    const uint32_t cnt = b < a.bins ? wh[b] : 0u;
+                    if (cnt) atomicAdd(&hb[b], (unsigned long long)cnt);
+                    const double p = (double)cnt * inv;
+                    if (cnt) ent -= p * log(p);
+                    double scan = p;  // inclusive prefix sum over the wave
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const double y = __shfl_up(scan, o, 64);
+                        if ((int)lane >= o) scan += y;
+                    }
+                    if (a.has_target && b < a.bins) ks = fmax(ks, fabs(carry + scan - a.target_cdf[b]));
+                    carry += __shfl(scan, 63, 64);
+                }
+                ent = wave_sum(ent);
+                ks = wave_max(ks);
+                if (lane == 0) {
+                    ecdna_rep_stats_t st;
+                    st.cells = cells;
+                    st.mean = cells ? (double)ksum * inv : 0.0;
+                    st.entropy = ent;
+                    st.frequency = cells ? (double)np * inv : 0.0;
+                    st.ks = a.has_target ? (cells ? ks : 1.0) : 0.0;
+                    const double dm = fabs(st.mean - a.target_mean), de = fabs(st.entropy - a.target_entropy);
+                    st.mean_rel = a.has_target ? (a.target_mean > 0.0 ? dm / a.target_mean : dm) : 0.0;
+                    st.entropy_rel = a.has_target ? (a.target_entropy > 0.0 ? de / a.target_entropy : de) : 0.0;
+                    st.frequency_diff = a.has_target ? fabs(st.frequency - a.target_freq) : 0.0;
+                    a.stats[q] = st;
+                }
+            }
             if (lane == 0) {
-                atomicAdd(&hb[0], (unsigned long long)s->nminus);
+                if (!STATS) atomicAdd(&hb[0], (unsigned long long)s->nminus);
                 atomicAdd(&tb[0], 1ull);
                 atomicAdd(&tb[1], (unsigned long long)s->iters);
                 atomicAdd(&tb[2], (unsigned long long)s->events_by_type[0]);
@@ -447,8 +518,10 @@ hipError_t launch_stepper(const StepperArgs& a, int birth_death, int segregation
 hipError_t launch_hist(const HistArgs& a, uint32_t blocks, hipStream_t stream) {
     HistArgs copy = a;
     void* args[] = {&copy};
-    const size_t lds = (size_t)(a.bins + 16) * sizeof(unsigned long long);
-    return hipLaunchKernel((const void*)ssa_hist, dim3(blocks), dim3(kHistBlock), args, lds, stream);
+    size_t lds = (size_t)(a.bins + 16) * sizeof(unsigned long long);
+    if (a.stats) lds += (size_t)(kHistBlock / 64) * a.bins * sizeof(uint32_t);  // per-wave replicate histograms
+    const void* k = a.stats ? (const void*)ssa_hist<true> : (const void*)ssa_hist<false>;
+    return hipLaunchKernel(k, dim3(blocks), dim3(kHistBlock), args, lds, stream);
 }
 
 }  // namespace ecdna

@@ -50,6 +50,11 @@ struct HistArgs {
     uint32_t n;
     uint32_t bins;
     uint32_t reps_per_block;
+    // per-replicate ABC statistics (nullptr = off), against target_cdf[bins] when has_target
+    ecdna_rep_stats_t* stats;             // chunk-offset
+    const double* target_cdf;
+    double target_mean, target_entropy, target_freq;
+    uint32_t has_target;
 };
 
 constexpr int kStepperBlock = 256;

@@ -14,7 +14,7 @@ from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # ecdna_process_t (ProcessType, src/clap_app.rs:311-315)
 PURE_BIRTH = 0
@@ -85,7 +85,14 @@ class Params(C.Structure):
         ("snapshot_cells", C.POINTER(C.c_uint64)),
         ("n_snapshots", C.c_uint32),
         ("reserved2", C.c_uint32),
+        ("stats_target_hist", C.POINTER(C.c_uint64)),
     ]
+
+
+STATS_DTYPE = np.dtype([("mean", "<f8"), ("entropy", "<f8"), ("frequency", "<f8"), ("ks", "<f8"),
+                        ("mean_rel", "<f8"), ("entropy_rel", "<f8"), ("frequency_diff", "<f8"), ("cells", "<u8")])
+assert STATS_DTYPE.itemsize == 64
+FLAG_REP_STATS = 0x10
 
 
 SNAPSHOT_DTYPE = np.dtype([("time", "<f8"), ("nminus", "<u8"), ("nplus", "<u8"), ("taken", "<u4"),
@@ -160,6 +167,7 @@ class RunSpec:
     init_per_set: Optional[List[Dict[int, int]]] = None
     device: int = 0
     snapshots: Optional[Sequence[int]] = None  # cell counts (sorted here); None = no snapshots
+    stats_target: Optional[Sequence[int]] = None  # target histogram [hist_bins] for ABC distances
     _keep: list = field(default_factory=list, repr=False)
 
     def resolved_max_time(self) -> float:
@@ -210,6 +218,12 @@ class RunSpec:
             self._keep.append(snaps)
             p.snapshot_cells = _ptr(snaps, C.c_uint64)
             p.n_snapshots = len(snaps)
+        if self.stats_target is not None:
+            tgt = np.asarray(self.stats_target, dtype=np.uint64)
+            if tgt.shape != (self.hist_bins,):
+                raise ValueError("stats_target must have hist_bins entries")
+            self._keep.append(tgt)
+            p.stats_target_hist = _ptr(tgt, C.c_uint64)
         max_np = 0
         if self.init_per_set is not None:
             if len(self.init_per_set) != n_sets:

@@ -33,6 +33,7 @@ EXPORTS = [
     "ecdna_ssa_ctx_device_outputs",
     "ecdna_ssa_ctx_download",
     "ecdna_ssa_ctx_download_snapshots",
+    "ecdna_ssa_ctx_download_stats",
     "ecdna_ssa_ctx_row_stride",
     "ecdna_ssa_ctx_geometry",
     "ecdna_ssa_ctx_destroy",
@@ -87,6 +88,8 @@ def lib():
     L.ecdna_ssa_ctx_download.restype = C.c_int
     L.ecdna_ssa_ctx_download_snapshots.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     L.ecdna_ssa_ctx_download_snapshots.restype = C.c_int
+    L.ecdna_ssa_ctx_download_stats.argtypes = [C.c_void_p, C.c_void_p]
+    L.ecdna_ssa_ctx_download_stats.restype = C.c_int
     L.ecdna_ssa_ctx_row_stride.argtypes = [C.c_void_p]
     L.ecdna_ssa_ctx_row_stride.restype = C.c_int64
     L.ecdna_ssa_ctx_geometry.argtypes = [C.c_void_p, P(C.c_uint64), P(C.c_uint64)]
@@ -119,6 +122,7 @@ class Result:
         self.row_stride = row_stride
         self.snapshots = None  # [n][S] abi.SNAPSHOT_DTYPE
         self.snapshot_rows = None  # [n][S][stride] u16 under FLAG_SNAPSHOT_ROWS
+        self.stats = None  # [n] abi.STATS_DTYPE under FLAG_REP_STATS
 
     def row(self, i: int) -> np.ndarray:
         return self.rows[i, : int(self.summaries[i]["nplus"])]
@@ -197,6 +201,10 @@ class Context:
                    "download_snapshots")
             res.snapshots = meta
             res.snapshot_rows = srows
+        if p.flags & abi.FLAG_REP_STATS:
+            st = np.zeros(p.n_replicates, dtype=abi.STATS_DTYPE)
+            _check(lib().ecdna_ssa_ctx_download_stats(self.h, st.ctypes.data), "download_stats")
+            res.stats = st
         return res
 
 

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ECDNA_SSA_ABI_VERSION 2
+#define ECDNA_SSA_ABI_VERSION 3
 
 /* Process type — ProcessType (src/clap_app.rs:311-315); chosen as BirthDeath
  * when d0 > 0 or d1 > 0 (src/clap_app.rs:163-174, 194-200). */
@@ -96,6 +96,7 @@ typedef enum {
                                           duplicated population vector (src/process.rs:339-344) */
 #define ECDNA_FLAG_EVENT_HASH 0x4u     /* fold every event into ecdna_rep_summary_t.event_hash */
 #define ECDNA_FLAG_SNAPSHOT_ROWS 0x8u  /* keep the N+ row of every snapshot (else only its metadata) */
+#define ECDNA_FLAG_REP_STATS 0x10u     /* per-replicate ABC statistics (ecdna_rep_stats_t) */
 
 /* API return codes. */
 #define ECDNA_OK 0
@@ -149,7 +150,24 @@ typedef struct {
     const uint64_t* snapshot_cells; /* host */
     uint32_t n_snapshots;
     uint32_t reserved2;
+    /* Per-replicate ABC summary statistics (abc.md:38-55; ECDNA_FLAG_REP_STATS): compared against this
+     * target copy-number histogram of hist_bins entries (bin 0 = N- cells, last bin = overflow), e.g.
+     * the patient's data. NULL: statistics are computed, distances to the target are not. */
+    const uint64_t* stats_target_hist; /* host */
 } ecdna_ssa_params_t;
+
+/* Per-replicate summary statistics of the final distribution (cells = n- + n+, copy number k per cell,
+ * k = 0 for N- cells; bins as in the histogram). Distances are against params.stats_target_hist. */
+typedef struct {
+    double mean;           /* sum k / cells                                           */
+    double entropy;        /* -sum_k p_k ln p_k, p_k = cells with k copies / cells     */
+    double frequency;      /* n+ / cells                                              */
+    double ks;             /* max_k |F(k) - F_target(k)|, F = cumulative p over bins  */
+    double mean_rel;       /* |mean - mean_t| / mean_t      (|mean - mean_t| if mean_t == 0) */
+    double entropy_rel;    /* |entropy - entropy_t| / entropy_t (likewise)            */
+    double frequency_diff; /* |frequency - frequency_t|                               */
+    uint64_t cells;
+} ecdna_rep_stats_t;
 
 /* One saved snapshot of one replicate (what process::save writes, src/process.rs:31-55). */
 typedef struct {
@@ -226,6 +244,8 @@ int ecdna_ssa_ctx_download(ecdna_ssa_ctx* c, ecdna_rep_summary_t* out_summaries,
  * rows[n_replicates][n_snapshots][row_stride] u16 (the N+ cells in swap_remove order at the save).
  * Either may be NULL. */
 int ecdna_ssa_ctx_download_snapshots(ecdna_ssa_ctx* c, ecdna_snapshot_t* meta, uint16_t* rows);
+/* Per-replicate statistics of the last launch (needs ECDNA_FLAG_REP_STATS): out[n_replicates]. */
+int ecdna_ssa_ctx_download_stats(ecdna_ssa_ctx* c, ecdna_rep_stats_t* out);
 /* Row stride (cells) of the rows buffer, or 0 when the run is chunked (rows not downloadable). */
 int64_t ecdna_ssa_ctx_row_stride(const ecdna_ssa_ctx* c);
 /* Replicates per chunk (memory bound) and lanes of the persistent stepper grid. */
