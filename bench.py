@@ -88,6 +88,11 @@ def cpu_baseline(threads: int):
 
 
 def main():
+    # exactly one JSON line on stdout: library chatter (e.g. RCCL's version banner, printed to fd 1 when a
+    # communicator is created) goes to stderr; the result line is written to the saved stdout
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -99,7 +104,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # under torchrun (even at one rank) the RCCL path runs: process group, all-reduce, barriers
+    distributed = "RANK" in os.environ and "MASTER_ADDR" in os.environ
+    if distributed:
         torch.cuda.set_device(local)
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
     else:
@@ -109,7 +116,7 @@ def main():
     total = reps * n_gpus
 
     first, n = shard.weak_range(rank, reps)
-    spec = workload_spec(first, n, total, device=local if world > 1 else 0)
+    spec = workload_spec(first, n, total, device=local if distributed else 0)
     ctx = engine.Context(spec)
     hist = torch.zeros(spec.hist_bins, dtype=torch.int64, device="cuda")
     tot = torch.zeros(16, dtype=torch.int64, device="cuda")
@@ -123,14 +130,14 @@ def main():
     def step():
         ctx.launch(stream)
         tot_local.copy_(tot)  # this GPU's totals, before the reduction
-        if world > 1:
+        if distributed:
             shard.reduce_outputs(hist, tot)
 
     for _ in range(args.warmup):
         step()
         ctx.sync()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -141,7 +148,7 @@ def main():
         kernel_ms.append(s_ms)
         hist_ms.append(h_ms)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -151,7 +158,7 @@ def main():
     local_alg = algorithmic_bytes(local_words, reps)
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     ev = torch.tensor([local_events], dtype=torch.int64, device="cuda")
-    if world > 1:
+    if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(ev)
     elapsed = float(t.item())
@@ -205,9 +212,9 @@ def main():
             },
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
     ctx.close()
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 
