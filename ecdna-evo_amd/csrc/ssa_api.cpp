@@ -108,7 +108,6 @@ struct ecdna_ssa_ctx {
     uint64_t chunk_reps = 0;
     uint32_t stepper_blocks_cap = 0;
     int window = 1;  // LDS tail window stepper (ECDNA_SSA_WINDOW=0 selects the HBM-only variant)
-    int prefetch = 1;  // speculative next-event load (ECDNA_SSA_PREFETCH=0 disables)
     // owned copies of the host inputs
     std::vector<ecdna_rates_t> rates;
     std::vector<uint16_t> init_copies;
@@ -355,10 +354,9 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
 
     // persistent stepper grid: as many resident lanes as the occupancy allows
     c->window = env_u64("ECDNA_SSA_WINDOW", 1) ? 1 : 0;
-    c->prefetch = env_u64("ECDNA_SSA_PREFETCH", 1) ? 1 : 0;
     int per_cu = 0;
     CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, ecdna::stepper_kernel(p->process, p->segregation, c->window ? 1 + c->prefetch : 0), ecdna::kStepperBlock, 0));
+        &per_cu, ecdna::stepper_kernel(p->process, p->segregation, c->window), ecdna::kStepperBlock, 0));
     // Memory-level parallelism of the random row accesses saturates HBM at about 3 resident 256-lane
     // blocks per CU (C3 sweep, DESIGN.md §8: 1/2/3/4/7 blocks -> 617/372/329/336/349 ms); fewer
     // lanes also mean more replicates per lane and a shorter drain once the work queue is empty.
@@ -418,20 +416,15 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
         a.cell_cap = p.cell_cap;
         a.flags = p.flags;
         a.cells_mul = (p.process == ECDNA_BIRTH_DEATH && (p.flags & ECDNA_FLAG_BD_CAP_COMPAT)) ? 2u : 1u;
-        a.prefetch = 0;
         a.n_snap = p.n_snapshots;
         a.snap_cells = c->d_snap_cells;
         a.snap_meta = c->d_snap_meta ? c->d_snap_meta + ch.first * p.n_snapshots : nullptr;
         a.snap_rows = c->d_snap_rows ? c->d_snap_rows + ch.first * p.n_snapshots * c->row_stride : nullptr;
         const uint32_t need = (ch.n + ecdna::kStepperBlock - 1) / ecdna::kStepperBlock;
         const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(need, c->stepper_blocks_cap));
-        // Variant 2 adds the speculative next-event load (channel-guessed, ProliferateNPlus only). It
-        // hides one HBM round trip per ProliferateNPlus; at C3 it measured 332 vs 338 ms, at a 65,536-
-        // replicate C3 shard 50.6 vs 51.9 ms, at C2 a tie. Default on.
-        const int variant = c->window ? (c->prefetch ? 2 : 1) : 0;
 
         HIP_TRY(hipEventRecord(ch.ev[0], st));
-        HIP_TRY(ecdna::launch_stepper(a, p.process, p.segregation, variant, blocks, st));
+        HIP_TRY(ecdna::launch_stepper(a, p.process, p.segregation, c->window, blocks, st));
         HIP_TRY(hipEventRecord(ch.ev[1], st));
 
         ecdna::HistArgs hsa{};

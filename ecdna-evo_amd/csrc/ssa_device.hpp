@@ -29,6 +29,9 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1
             k0 += kPhiloxW0;
             k1 += kPhiloxW1;
         }
+        // keep the round keys a per-call chain of scalar adds: hoisted out of the event loop they
+        // are 18 loop-invariant SGPRs, which spill to VGPR lanes (v_readlane in every event)
+        asm volatile("" : "+s"(k0), "+s"(k1));
         const uint64_t p0 = (uint64_t)kPhiloxM0 * c.x;
         const uint64_t p1 = (uint64_t)kPhiloxM1 * c.z;
         c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1,

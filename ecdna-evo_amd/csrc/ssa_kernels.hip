@@ -45,9 +45,8 @@ __device__ __forceinline__ uint32_t gload_u16(const uint16_t* p) {
 constexpr uint32_t kWin = 32;
 constexpr uint32_t kFlush = 16;
 
-template <bool BD, int SEG, bool WIN, bool PF>
+template <bool BD, int SEG, bool WIN>
 __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a) {
-    static_assert(WIN || !PF, "the speculative load needs the window variant");
     __shared__ uint16_t win[WIN ? kWin + 1 : 1][kStepperBlock];  // + 1 spare row
     const uint32_t tid = threadIdx.x;
     const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
@@ -60,17 +59,6 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
     uint16_t* row = a.rows;  // (not nullptr: keeps the pointer provably global, no flat_* accesses)
     uint32_t nm = 0, np = 0, tail = 0, wb = 0;
     bool tail_ok = false;
-    // Speculative next-event load (PF, window variant only): Philox is counter-based, so event e+1's words
-    // are known during event e; with n+ guessed from event e's channel (exact unless the split turns out
-    // uneven) its Lemire cell index is known too, and that HBM cell is loaded while event e runs. The
-    // value is used at e+1 only if the index matches and no write of event e touched that cell. The
-    // load is issued only when event e+1's channel, computed from the guessed populations, is a
-    // ProliferateNPlus (the only channel that reads a random cell).
-    constexpr uint32_t kNoSpec = 0xffffffffu;
-    uint32_t spec_idx = kNoSpec, spec_val = 0;
-    uint4 wnext = make_uint4(0, 0, 0, 0);
-    bool have_w = false;
-
     // cell access through the window (WIN) or straight to HBM
     auto slot = [&](uint32_t pos) -> uint16_t& { return win[WIN ? (pos & (kWin - 1)) : 0][tid]; };
     // LDS side unconditional (a spare row absorbs stores outside the window), HBM side under the
@@ -90,7 +78,6 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
         win[in_win ? (pos & (kWin - 1)) : kWin][tid] = (uint16_t)v;
         if (!in_win) {
             row[pos] = (uint16_t)v;
-            if (pos == spec_idx) spec_idx = kNoSpec;  // the speculated value is stale now
         }
     };
     auto flush_block = [&]() {  // cells [wb, wb + 16) -> HBM as two 16-B stores; wb += 16
@@ -176,8 +163,6 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
             stop = 0;
             err = 0;
             sj = 0;
-            spec_idx = kNoSpec;
-            have_w = false;
             if (np == 0 && nm == 0) {  // ensure!(!distribution.is_empty()) src/process.rs:88, 232
                 err = ECDNA_REP_ERR_EMPTY;
                 stop = ECDNA_STOP_ERROR;
@@ -250,11 +235,7 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
         }
 
         const uint32_t rid_lo = (uint32_t)rid, rid_hi = (uint32_t)(rid >> 32);
-        uint4 w;
-        if (PF && have_w)
-            w = wnext;  // computed during the previous event
-        else
-            w = philox4x32_10(make_uint4(e, 0u, rid_lo, rid_hi), k0, k1);
+        const uint4 w = philox4x32_10(make_uint4(e, 0u, rid_lo, rid_hi), k0, k1);
         const double target = (((double)w.y + 0.5) * 0x1p-32) * a0;
         uint32_t ch;
         if (BD)
@@ -290,48 +271,22 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
             if (ch == 1u) {
                 if (idx == np - 1)
                     k = tail;
-                else if (PF && idx == spec_idx && idx < wb)
-                    k = spec_val;  // speculated during the previous event, still valid
                 else
                     k = cell_get(idx);
             }
         }
 
-        if (PF) {  // speculate event e+1: its words, its populations, its channel and its cell
-            wnext = philox4x32_10(make_uint4(e + 1u, 0u, rid_lo, rid_hi), k0, k1);
-            have_w = true;
-            const uint32_t np_g = np + (ch == 1u ? 1u : 0u) - (ch == 3u ? 1u : 0u);  // even split assumed
-            const uint32_t nm_g = nm + (ch == 0u ? 1u : 0u) - (ch == 2u ? 1u : 0u);
-            const double ga = (double)b0 * (double)nm_g;
-            const double gb = ga + (double)b1 * (double)np_g;
-            double g0 = gb;
-            if (BD) g0 = (gb + (double)d0 * (double)nm_g) + (double)d1 * (double)np_g;
-            const double gt = (((double)wnext.y + 0.5) * 0x1p-32) * g0;
-            spec_idx = kNoSpec;
-            if (np_g && !(gt < ga) && gt < gb) {  // the next event is (probably) a ProliferateNPlus
-                const uint64_t m = (uint64_t)wnext.z * np_g;
-                const uint32_t sidx = (uint32_t)(m >> 32);
-                if ((uint32_t)m >= np_g && sidx < wb) {  // Lemire fast path, cell in HBM
-                    spec_idx = sidx;
-                    spec_val = gload_u16(row + sidx);
-                }
-            }
-        }
-
-        // waiting time: independent of the loads above, hides their latency
-        const double tau = softlog_neg(w.x) / a0;
-
-        uint64_t x = ch;
-        if (ch == 1u) {  // Exponential::increase_nplus (src/proliferation.rs:25-111)
+        // Exponential::increase_nplus (src/proliferation.rs:25-111): its draws and error checks
+        uint32_t n = 0, k1v = 0;
+        uint32_t un = 0;  // 0 False, 1 True, 2 TrueWithoutNMinusIncrease
+        if (ch == 1u) {
             if (k > 32767u) {  // checked_mul panic (src/proliferation.rs:63-67)
                 err = ECDNA_REP_ERR_OVERFLOW;
                 stop = ECDNA_STOP_ERROR;
                 active = false;
                 continue;
             }
-            const uint32_t n = 2u * k;
-            uint32_t k1v;
-            uint32_t un = 0;  // 0 False, 1 True, 2 TrueWithoutNMinusIncrease
+            n = 2u * k;
             if (SEG == ECDNA_SEG_DETERMINISTIC) {
                 k1v = k;
             } else {
@@ -368,7 +323,16 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
                 active = false;
                 continue;
             }
-            if (idx != np - 1) cell_put(idx, tail);  // swap_remove(idx)
+        }
+
+        // waiting time
+        const double tau = softlog_neg(w.x) / a0;
+
+        uint64_t x = ch;
+        if (ch == 1u) {
+            // swap_remove(idx); the slot already holds the tail's copy number about 7 % of the time at
+            // C3 (sum of p_k^2), and random HBM stores are the stepper's binding limit
+            if (idx != np - 1 && k != tail) cell_put(idx, tail);
             if (un == 0u) {
                 cell_put(np - 1, k1v);  // push k1, push k2
                 if (WIN && np - wb == kWin) flush_block();
@@ -543,26 +507,23 @@ __global__ void __launch_bounds__(kHistBlock) ssa_hist(const HistArgs a) {
 
 // ---------------------------------------------------------------- launch
 
-#define ECDNA_STEPPER_TABLE(BD, WIN, PF)                                                                    \
-    {(const void*)ssa_stepper<BD, 0, WIN, PF>, (const void*)ssa_stepper<BD, 1, WIN, PF>,                     \
-     (const void*)ssa_stepper<BD, 2, WIN, PF>, (const void*)ssa_stepper<BD, 3, WIN, PF>}
+#define ECDNA_STEPPER_TABLE(BD, WIN)                                                                        \
+    {(const void*)ssa_stepper<BD, 0, WIN>, (const void*)ssa_stepper<BD, 1, WIN>,                             \
+     (const void*)ssa_stepper<BD, 2, WIN>, (const void*)ssa_stepper<BD, 3, WIN>}
 
-// [variant][birth_death][segregation]; variant 0 = rows in HBM only, 1 = LDS tail window,
-// 2 = LDS tail window + speculative next-event load
-static const void* const kStepperTable[3][2][4] = {
-    {ECDNA_STEPPER_TABLE(false, false, false), ECDNA_STEPPER_TABLE(true, false, false)},
-    {ECDNA_STEPPER_TABLE(false, true, false), ECDNA_STEPPER_TABLE(true, true, false)},
-    {ECDNA_STEPPER_TABLE(false, true, true), ECDNA_STEPPER_TABLE(true, true, true)}};
+static const void* const kStepperTable[2][2][4] = {
+    {ECDNA_STEPPER_TABLE(false, false), ECDNA_STEPPER_TABLE(true, false)},
+    {ECDNA_STEPPER_TABLE(false, true), ECDNA_STEPPER_TABLE(true, true)}};
 
-const void* stepper_kernel(int birth_death, int segregation, int variant) {
-    return kStepperTable[variant < 0 ? 0 : (variant > 2 ? 2 : variant)][birth_death ? 1 : 0][segregation & 3];
+const void* stepper_kernel(int birth_death, int segregation, int window) {
+    return kStepperTable[window ? 1 : 0][birth_death ? 1 : 0][segregation & 3];
 }
 
-hipError_t launch_stepper(const StepperArgs& a, int birth_death, int segregation, int variant, uint32_t blocks,
+hipError_t launch_stepper(const StepperArgs& a, int birth_death, int segregation, int window, uint32_t blocks,
                           hipStream_t stream) {
     StepperArgs copy = a;
     void* args[] = {&copy};
-    return hipLaunchKernel(stepper_kernel(birth_death, segregation, variant), dim3(blocks), dim3(kStepperBlock), args,
+    return hipLaunchKernel(stepper_kernel(birth_death, segregation, window), dim3(blocks), dim3(kStepperBlock), args,
                            0, stream);
 }
 

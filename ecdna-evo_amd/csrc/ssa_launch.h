@@ -32,7 +32,6 @@ struct StepperArgs {
     uint32_t cell_cap;
     uint32_t flags;
     uint32_t cells_mul;             // 2 under ECDNA_FLAG_BD_CAP_COMPAT for birth-death, else 1
-    uint32_t prefetch;              // unused (the speculative load is the compile-time variant 2)
     uint32_t n_snap;                // snapshots (0 = none)
     const uint64_t* snap_cells;     // [n_snap], ascending
     ecdna_snapshot_t* snap_meta;    // [n][n_snap], chunk-offset
@@ -64,10 +63,9 @@ constexpr uint32_t kMaxHistBins = 4096;  // LDS: 8 B per bin per workgroup (<= 6
 constexpr uint32_t kMaxSnapshots = 64;
 
 // Kernel handle for occupancy queries and the launch itself.
-// variant: 0 = rows straight in HBM (A/B reference), 1 = LDS tail window (default),
-//          2 = LDS tail window + speculative load of the next event's cell
-const void* stepper_kernel(int birth_death, int segregation, int variant);
-hipError_t launch_stepper(const StepperArgs& a, int birth_death, int segregation, int variant, uint32_t blocks,
+// window: 1 = LDS tail window variant (default), 0 = rows straight in HBM (A/B reference)
+const void* stepper_kernel(int birth_death, int segregation, int window);
+hipError_t launch_stepper(const StepperArgs& a, int birth_death, int segregation, int window, uint32_t blocks,
                           hipStream_t stream);
 hipError_t launch_hist(const HistArgs& a, uint32_t blocks, hipStream_t stream);
 

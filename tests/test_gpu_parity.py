@@ -85,20 +85,6 @@ def test_gpu_grid_size_does_not_change_results(engine_mod, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["pb_binomial_c1", "bd_binomial", "bd_shrink", "bd_turnover", "big_copies",
-                                  "bd_snapshots", "overflow"])
-@pytest.mark.parametrize("prefetch", ["0", "1"])
-def test_gpu_forced_speculative_load_setting_matches_oracle(name, prefetch, engine_mod, oracle_mod, monkeypatch):
-    """The speculative next-event load (default on) changes no result: forced off
-    (ECDNA_SSA_PREFETCH=0) and forced on with lane refill (=1, one block) are both exact."""
-    monkeypatch.setenv("ECDNA_SSA_PREFETCH", prefetch)
-    if prefetch == "1":
-        monkeypatch.setenv("ECDNA_SSA_MAX_BLOCKS", "1")
-    spec = CASES[name]
-    _compare(engine_mod.run(spec, want_rows=True), oracle_mod.run(spec, mode="philox", want_rows=True), name)
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("name", ["pb_binomial_c1", "bd_binomial", "bd_shrink", "bd_turnover", "big_copies", "abc_sets"])
 def test_gpu_hbm_only_variant_matches_oracle(name, engine_mod, oracle_mod, monkeypatch):
     """The A/B reference variant without the LDS tail window (ECDNA_SSA_WINDOW=0) is exact too."""

@@ -74,3 +74,4 @@ def test_random_specs_are_valid_for_the_oracle(oracle_mod):
             spec.first_replicate = 0
             spec.n_replicates = spec.reps_per_set * len(spec.rates)
         oracle_mod.run(spec, mode="philox")
+
