@@ -415,7 +415,10 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
         a.max_iter = (uint32_t)p.max_iter;
         a.cell_cap = p.cell_cap;
         a.flags = p.flags;
-        a.cells_mul = (p.process == ECDNA_BIRTH_DEATH && (p.flags & ECDNA_FLAG_BD_CAP_COMPAT)) ? 2u : 1u;
+        // (n- + n+) * 2 >= max_cells  <=>  n- + n+ >= ceil(max_cells / 2)
+        a.stop_cells = (p.process == ECDNA_BIRTH_DEATH && (p.flags & ECDNA_FLAG_BD_CAP_COMPAT))
+                           ? p.max_cells / 2 + (p.max_cells & 1)
+                           : p.max_cells;
         a.n_snap = p.n_snapshots;
         a.snap_cells = c->d_snap_cells;
         a.snap_meta = c->d_snap_meta ? c->d_snap_meta + ch.first * p.n_snapshots : nullptr;

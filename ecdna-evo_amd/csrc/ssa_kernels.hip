@@ -58,7 +58,7 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
     uint64_t rid = 0;
     uint16_t* row = a.rows;  // (not nullptr: keeps the pointer provably global, no flat_* accesses)
     uint32_t nm = 0, np = 0, tail = 0, wb = 0;
-    bool tail_ok = false;
+    bool tail_ok = false;  // (HBM-only variant: tail value cached; the window variant always has it)
     // cell access through the window (WIN) or straight to HBM
     auto slot = [&](uint32_t pos) -> uint16_t& { return win[WIN ? (pos & (kWin - 1)) : 0][tid]; };
     // LDS side unconditional (a spare row absorbs stores outside the window), HBM side under the
@@ -156,6 +156,7 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
             np = cnt;
             nm = (uint32_t)(a.init_nminus_set ? a.init_nminus_set[set] : a.init_nminus);
             tail_ok = false;
+            if (WIN && cnt) tail = src[cnt - 1];
             t = 0.0;
             t32 = 0.f;
             e = n_pm = n_pp = n_dm = n_dp = n_un = 0;
@@ -184,18 +185,13 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
             a0 = cC + pd;
         }
 
-        // stop checks, in the order of DESIGN.md §3.1
+        // stop checks, in the order of DESIGN.md §3.1 (selects, last write = first check)
         {
-            const uint64_t cells = ((uint64_t)nm + np) * a.cells_mul;
-            uint32_t s = 0;
-            if (e >= a.max_iter)
-                s = ECDNA_STOP_MAX_ITER;
-            else if (cells >= a.max_cells)
-                s = ECDNA_STOP_MAX_CELLS;
-            else if (f32t ? (t32 >= a.max_time32) : (t >= a.max_time))
-                s = ECDNA_STOP_MAX_TIME;
-            else if (!(a0 > 0.0))
-                s = ECDNA_STOP_ABSORBING;
+            const bool t_over = f32t ? (t32 >= a.max_time32) : (t >= a.max_time);
+            uint32_t s = (a0 > 0.0) ? 0u : (uint32_t)ECDNA_STOP_ABSORBING;
+            s = t_over ? (uint32_t)ECDNA_STOP_MAX_TIME : s;
+            s = ((uint64_t)nm + np >= a.stop_cells) ? (uint32_t)ECDNA_STOP_MAX_CELLS : s;
+            s = (e >= a.max_iter) ? (uint32_t)ECDNA_STOP_MAX_ITER : s;
             if (s) {
                 stop = s;
                 active = false;
@@ -229,7 +225,7 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
             }
         }
 
-        if (!tail_ok && np > 0) {  // refill the cached tail value (after a DeathNPlus)
+        if (!WIN && !tail_ok && np > 0) {  // reload the cached tail value (after a DeathNPlus)
             tail = cell_get(np - 1);
             tail_ok = true;
         }
@@ -333,38 +329,37 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
             // swap_remove(idx); the slot already holds the tail's copy number about 7 % of the time at
             // C3 (sum of p_k^2), and random HBM stores are the stepper's binding limit
             if (idx != np - 1 && k != tail) cell_put(idx, tail);
+            // the pushes land at np - 1 and np, inside the window (np - wb >= 1 before, <= 32 after a flush)
             if (un == 0u) {
-                cell_put(np - 1, k1v);  // push k1, push k2
+                if (WIN) slot(np - 1) = (uint16_t)k1v; else cell_put(np - 1, k1v);  // push k1, push k2
                 if (WIN && np - wb == kWin) flush_block();
-                cell_put(np, n - k1v);
+                if (WIN) slot(np) = (uint16_t)(n - k1v); else cell_put(np, n - k1v);
                 np += 1;
                 tail = n - k1v;
             } else {
-                cell_put(np - 1, n);  // push k1 + k2
+                if (WIN) slot(np - 1) = (uint16_t)n; else cell_put(np - 1, n);  // push k1 + k2
                 tail = n;
-                if (un == 1u) nm += 1;
+                nm += (un == 1u) ? 1u : 0u;
                 n_un += 1;
             }
             x |= ((uint64_t)k1v << 2) | ((uint64_t)idx << 20);
-            n_pp += 1;
         } else if (BD && ch == 3u) {  // CellDeath::decrease_nplus (src/proliferation.rs:126-133)
             if (idx != np - 1) cell_put(idx, tail);
             np -= 1;
             if (WIN) {
                 if (np > 0 && np == wb) refill_block();  // keep the window non-empty
-                tail_ok = false;  // re-read from LDS at the next event
+                if (np > 0) tail = slot(np - 1);
             } else {
                 tail_ok = (np > 0) && (idx == np - 1);
             }
             x |= (uint64_t)idx << 20;
-            n_dp += 1;
-        } else if (ch == 0u) {  // increase_nminus (src/proliferation.rs:113-117)
-            nm += 1;
-            n_pm += 1;
-        } else {  // decrease_nminus (src/proliferation.rs:135-139)
-            nm -= 1;
-            n_dm += 1;
         }
+        // increase_nminus / decrease_nminus (src/proliferation.rs:113-117, 135-139) and the counters
+        nm = nm + (ch == 0u ? 1u : 0u) - (ch == 2u ? 1u : 0u);
+        n_pm += ch == 0u ? 1u : 0u;
+        n_pp += ch == 1u ? 1u : 0u;
+        n_dm += ch == 2u ? 1u : 0u;
+        n_dp += ch == 3u ? 1u : 0u;
         e += 1;
         if (f32t)
             t32 = t32 + (float)tau;

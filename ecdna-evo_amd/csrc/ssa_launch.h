@@ -23,6 +23,8 @@ struct StepperArgs {
     uint64_t rid0;                  // global id of the chunk's first replicate
     uint64_t reps_per_set;
     uint64_t max_cells;
+    uint64_t stop_cells;            // MaxCells when n- + n+ >= stop_cells: max_cells, or
+                                    // ceil(max_cells / 2) under ECDNA_FLAG_BD_CAP_COMPAT (birth-death)
     uint64_t init_nminus;
     double max_time;
     float max_time32;
@@ -31,7 +33,6 @@ struct StepperArgs {
     uint32_t max_iter;
     uint32_t cell_cap;
     uint32_t flags;
-    uint32_t cells_mul;             // 2 under ECDNA_FLAG_BD_CAP_COMPAT for birth-death, else 1
     uint32_t n_snap;                // snapshots (0 = none)
     const uint64_t* snap_cells;     // [n_snap], ascending
     ecdna_snapshot_t* snap_meta;    // [n][n_snap], chunk-offset
