@@ -14,7 +14,10 @@ resident in HBM before the timed region.
 Extra JSON fields:
   roofline      — the stepper kernel against HBM: algorithmic bytes per launch over
                   its average duration (HIP events on the launch stream), vs 8 TB/s; `traffic` =
-                  measured HBM bytes per launch from the committed rocprofv3 PMC summary, if present.
+                  measured HBM bytes per launch from the committed rocprofv3 PMC summary, if present;
+                  `hbm_requests` = the same kernel against the random-access request ceiling that
+                  actually bounds it (requests per event from the PMC summary x events/s, vs the
+                  calibrated random read-modify-write rate).
   cpu_baseline  — the reference-semantics CPU restatement (oracle/, ChaCha8 + first-reaction +
                   BTPE, "port") on a bounded sample of the same workload, rank 0 at N=1 only.
 """
@@ -54,15 +57,28 @@ def algorithmic_bytes(words, n_reps: int, init_cells: int = 1) -> int:
             + n_reps * (2 * init_cells + B_SUMMARY))
 
 
-def load_traffic(n_gpus: int):
-    """Measured HBM bytes per stepper launch (rocprofv3 PMC, corrected; profiles/pmc_c3.json)."""
-    p = os.path.join(REPO, "profiles", "pmc_c3.json")
+def load_pmc():
+    """The committed rocprofv3 PMC summary of the stepper on this workload (profiles/pmc_c3.json)."""
     try:
-        with open(p) as f:
-            d = json.load(f)
-        return d.get("hbm_bytes_per_launch")
+        with open(os.path.join(REPO, "profiles", "pmc_c3.json")) as f:
+            return json.load(f)
     except Exception:
-        return None
+        return {}
+
+
+def rmw_ceiling():
+    """Random 2-B read-modify-write pairs/s the chip sustains (tools/rmw_shapes.hip, 4 GiB buffer,
+    best lane count; profiles/r01d_access_microbench.jsonl)."""
+    best = None
+    try:
+        with open(os.path.join(REPO, "profiles", "r01d_access_microbench.jsonl")) as f:
+            for line in f:
+                d = json.loads(line)
+                if d.get("shape") == "rmw_u16":
+                    best = max(best or 0.0, d["ops_per_s"])
+    except Exception:
+        pass
+    return best
 
 
 def cpu_baseline(threads: int):
@@ -171,7 +187,22 @@ def main():
     if rank == 0:
         avg_kernel_s = sum(kernel_ms) / len(kernel_ms) * 1e-3
         achieved = local_alg / avg_kernel_s / 1e9
-        traffic = load_traffic(n_gpus)
+        pmc = load_pmc()
+        traffic = pmc.get("hbm_bytes_per_launch")
+        kernel_eps = local_events / avg_kernel_s
+        transactions = None
+        if "read_requests_per_event" in pmc:
+            per_event = pmc["read_requests_per_event"] + pmc["write_requests_per_event"]
+            ceiling = rmw_ceiling()
+            transactions = {
+                "requests_per_event": per_event,
+                "per_s": per_event * kernel_eps,
+                "random_rmw_ceiling_per_s": 2 * ceiling if ceiling else None,
+                "frac": per_event * kernel_eps / (2 * ceiling) if ceiling else None,
+                "note": "random 2-B cell accesses move whole 64-B read / 32-B write requests, so the "
+                        "stepper is bounded by HBM request rate, not bytes (DESIGN.md §5); requests per "
+                        "event from the committed PMC summary, ceiling from tools/rmw_shapes.hip",
+            }
         cpu = None
         if n_gpus == 1 and not args.no_cpu_baseline:
             threads = int(os.environ.get("ECDNA_BENCH_CPU_THREADS", "0")) or min(16, os.cpu_count() or 1)
@@ -200,7 +231,7 @@ def main():
                 "grid_lanes": lanes,
                 "kernel_ms_avg": avg_kernel_s * 1e3,
                 "hist_kernel_ms_avg": sum(hist_ms) / len(hist_ms),
-                "kernel_events_per_s_per_gpu": local_events / avg_kernel_s,
+                "kernel_events_per_s_per_gpu": kernel_eps,
             },
             "roofline": {
                 "bound": "hbm",
@@ -209,6 +240,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "hbm_requests": transactions,
             },
             "cpu_baseline": cpu,
         }
