@@ -97,10 +97,19 @@ def cpu_baseline(threads: int):
     r = oracle.run(spec, mode="compat", n_threads=threads)
     dt = time.time() - t0
     ev = int(r.totals["events"].sum())
+    # for information: the same sample through the engine's own draw mapping on the CPU
+    n_ph = max(1024, n // 2)
+    t0 = time.time()
+    rp = oracle.run(workload_spec(0, n_ph, REPS_PER_GPU), mode="philox", n_threads=threads)
+    dt_ph = time.time() - t0
+    ev_ph = int(rp.totals["events"].sum())
     return {"value": ev / dt, "unit": "events/s", "cores": threads, "kind": "port",
             "sample": f"C3 shape, replicates 0..{n - 1} of 2^20 ({ev} events, {dt:.1f} s wall), "
                       f"oracle compat mode (ChaCha8 streams seed*10+i, first-reaction, BTPE), "
-                      f"{threads} threads"}
+                      f"{threads} threads",
+            "philox_mode_value": ev_ph / dt_ph,
+            "philox_mode_sample": f"replicates 0..{n_ph - 1}, oracle philox mode (the engine's draw mapping, "
+                                  f"direct method, popcount binomial), {threads} threads"}
 
 
 def main():

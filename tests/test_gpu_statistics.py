@@ -42,6 +42,44 @@ def _invariants(res, spec):
     assert np.all(np.bincount(s["stop_reason"], minlength=6) == t["stop_reasons"].sum(axis=0))
 
 
+def _balance(res, init_nplus, init_nminus=0):
+    """Population bookkeeping per replicate under Binomial segregation (src/proliferation.rs:81-117,
+    125-140): every ProliferateNMinus adds an N- cell, every uneven split (IsUneven::True) turns one
+    N+ cell into an N+ and an N- cell, every even split adds one N+ cell, deaths remove one."""
+    s = res.summaries
+    ev = s["events_by_type"].astype(np.int64)
+    un = s["uneven"].astype(np.int64)
+    np.testing.assert_array_equal(s["nminus"].astype(np.int64), init_nminus + ev[:, 0] - ev[:, 2] + un)
+    np.testing.assert_array_equal(s["nplus"].astype(np.int64), init_nplus + ev[:, 1] - un - ev[:, 3])
+
+
+def c4_shard_spec(rank=0, gpus=8, **kw):
+    """C4 (BASELINE.json configs[3]): 1024 (b1, d, k0) parameter sets x 4096 replicates over 8 GPUs;
+    this is rank `rank`'s shard of 128 whole sets."""
+    rates, inits = [], []
+    for i in range(1024):
+        sel = 1.0 + 1.5 * (i % 16) / 15.0
+        d = 0.7 * ((i // 16) % 8) / 7.0
+        rates.append((1.0, sel, d, d))
+        inits.append({1 << (i // 128): 1})
+    n = 1024 * 4096 // gpus
+    d = dict(seed=42, process=abi.BIRTH_DEATH, rates=rates, reps_per_set=4096, first_replicate=rank * n,
+             n_replicates=n, max_cells=10_000, init_per_set=inits, hist_bins=1025, flags=0)
+    d.update(kw)
+    return abi.RunSpec(**d)
+
+
+def c5_shard_spec(rank=0, gpus=8, **kw):
+    """C5 (BASELINE.json configs[4]): 262,144 turnover replicates from 1,000 cells to 1e6 cells or
+    t = 1000 over 8 GPUs; this is rank `rank`'s shard of 32,768 replicates."""
+    n = 262_144 // gpus
+    d = dict(seed=42, process=abi.BIRTH_DEATH, rates=((1.0, 1.0, 0.9, 0.9),), reps_per_set=262_144,
+             first_replicate=rank * n, n_replicates=n, max_cells=1_000_000, max_time=1000.0, init={1: 1000},
+             hist_bins=1025, flags=0)
+    d.update(kw)
+    return abi.RunSpec(**d)
+
+
 @pytest.mark.gpu
 def test_c2_ks_against_reference_semantics(engine_mod):
     """C2 shape (65,536 replicates, pure birth + binomial to 1e4 cells, seed 42) on the GPU vs the
@@ -49,6 +87,7 @@ def test_c2_ks_against_reference_semantics(engine_mod):
     g = np.load(os.path.join(GOLDEN, "c2_compat_seed42.npz"))
     r = engine_mod.run(c2_spec())
     _invariants(r, c2_spec())
+    _balance(r, 1)
     ks = _ks(r.hist[0], g["hist"])
     assert ks < KS_TOL, ks
     # per-replicate law of the N- fraction (two-sample KS on replicates, not cells)
@@ -75,6 +114,7 @@ def test_c3_full_size_properties_and_shard_identity(engine_mod):
     reproduce the full run's summaries and histogram bit for bit (the 1-GPU == N-GPU identity)."""
     full = engine_mod.run(c3_spec())
     _invariants(full, c3_spec())
+    _balance(full, 1)
     half = 1 << 19
     a = engine_mod.run(c3_spec(0, half))
     b = engine_mod.run(c3_spec(half, half))
@@ -134,3 +174,36 @@ def test_abc_sweep_shape_small(engine_mod, oracle_mod):
     np.testing.assert_array_equal(g.hist, c.hist)
     np.testing.assert_array_equal(g.summaries["event_hash"], c.summaries["event_hash"])
     assert np.all(g.totals["replicates"] == 32)
+
+
+@pytest.mark.gpu
+def test_c4_shard_full_size_properties(engine_mod, oracle_mod):
+    """C4 rank-0 shard at full size (524,288 replicates, 128 parameter sets with per-set rates and
+    initial copy numbers): invariants, bookkeeping, per-set replicate counts, and 256 replicates of a
+    birth-death set with initial k = 1 against the oracle bit for bit (event hash)."""
+    spec = c4_shard_spec(flags=abi.FLAG_EVENT_HASH)
+    r = engine_mod.run(spec)
+    _invariants(r, spec)
+    _balance(r, 1)
+    assert np.all(r.totals["replicates"][:128] == 4096) and np.all(r.totals["replicates"][128:] == 0)
+    first = 37 * 4096  # set 37: b1 = 1.2, d = 0.2, k0 = 1
+    c = oracle_mod.run(c4_shard_spec(first_replicate=first, n_replicates=256, flags=abi.FLAG_EVENT_HASH),
+                       mode="philox")
+    for f in c.summaries.dtype.names:
+        np.testing.assert_array_equal(r.summaries[f][first:first + 256], c.summaries[f], err_msg=f)
+
+
+@pytest.mark.gpu
+def test_c5_shard_full_size_properties(engine_mod, oracle_mod):
+    """C5 rank-0 shard at full size (32,768 replicates, rows up to 1e6 cells = 2 MB, 65 GB of rows):
+    invariants, bookkeeping, the stop law of a critical-ish turnover process, and replicates 0..3
+    (about 2e7 events each) against the oracle bit for bit (event hash)."""
+    spec = c5_shard_spec(flags=abi.FLAG_EVENT_HASH)
+    r = engine_mod.run(spec)
+    _invariants(r, spec)
+    _balance(r, 1000)
+    stops = set(r.summaries["stop_reason"].tolist())
+    assert stops <= {abi.STOP_MAX_CELLS, abi.STOP_MAX_TIME, abi.STOP_ABSORBING}, stops
+    c = oracle_mod.run(c5_shard_spec(n_replicates=4, flags=abi.FLAG_EVENT_HASH), mode="philox", n_threads=4)
+    for f in c.summaries.dtype.names:
+        np.testing.assert_array_equal(r.summaries[f][:4], c.summaries[f], err_msg=f)
