@@ -18,7 +18,8 @@ import numpy as np
 from . import abi
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # .../ecdna-evo_amd
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libecdna_ssa.so")
+# ECDNA_SSA_LIB: development override (same-box A/B of two builds, tools/ab_build.sh)
+LIB_PATH = os.environ.get("ECDNA_SSA_LIB") or os.path.join(PKG_ROOT, "lib", "libecdna_ssa.so")
 
 EXPORTS = [
     "ecdna_ssa_abi_version",
