@@ -3,6 +3,7 @@
 #include <cstring>
 #include <string>
 
+#include "../../include/ecdna_host.h"
 #include "ecdna_host.hpp"
 
 namespace {

@@ -34,6 +34,17 @@ def host():
     return L
 
 
+def test_host_library_exports_every_declared_symbol(host):
+    import re
+
+    with open(os.path.join(REPO, "include", "ecdna_host.h")) as f:
+        text = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
+    names = sorted(set(re.findall(r"\b(ecdna_host_\w+)\s*\(", text)))
+    assert len(names) == 6
+    for n in names:
+        assert hasattr(host, n), f"libecdna_host.so does not export {n}"
+
+
 def _s(fn, *args):
     buf = C.create_string_buffer(512)
     assert fn(*args, buf, 512) >= 0
