@@ -74,6 +74,8 @@ int validate(const ecdna_ssa_params_t* p) {
     if (p->n_replicates && (p->first_replicate + p->n_replicates - 1) / p->reps_per_set >= p->n_param_sets)
         return fail(ECDNA_E_INVALID, "replicate ids map past the last parameter set");
     if (p->cell_cap == 0) return fail(ECDNA_E_INVALID, "cell_cap must be >= 1");
+    if ((p->flags & ECDNA_FLAG_BIN_STORE) && p->bin_kmax != 0 && p->bin_kmax != 64 && p->bin_kmax != 256)
+        return fail(ECDNA_E_INVALID, "bin_kmax must be 0 (= 64), 64 or 256");
     if (p->n_snapshots > ecdna::kMaxSnapshots) return fail(ECDNA_E_INVALID, "at most 64 snapshots");
     if (p->n_snapshots && !p->snapshot_cells) return fail(ECDNA_E_INVALID, "snapshot_cells is NULL");
     for (uint32_t q = 1; q < p->n_snapshots; ++q)
@@ -108,6 +110,12 @@ struct ecdna_ssa_ctx {
     uint64_t chunk_reps = 0;
     uint32_t stepper_blocks_cap = 0;
     int window = 1;  // LDS tail window stepper (ECDNA_SSA_WINDOW=0 selects the HBM-only variant)
+    // bin store (ECDNA_FLAG_BIN_STORE): binned copy numbers (0 = row store), u32 counters, the
+    // per-replicate final counters [chunk_reps][bin_k]
+    uint32_t bin_k = 0;
+    int bin_c32 = 0;
+    void* d_bags = nullptr;
+    uint32_t stepper_block = ecdna::kStepperBlock;
     // owned copies of the host inputs
     std::vector<ecdna_rates_t> rates;
     std::vector<uint16_t> init_copies;
@@ -175,6 +183,7 @@ void free_ctx(ecdna_ssa_ctx* c) {
     (void)hipFree(c->d_target_cdf);
     (void)hipFree(c->d_stats);
     (void)hipFree(c->d_rows);
+    (void)hipFree(c->d_bags);
     (void)hipFree(c->d_summ);
     (void)hipFree(c->d_heads);
     (void)hipFree(c->d_hist_own);
@@ -322,6 +331,12 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
     CTX_TRY(hipMalloc(&c->d_summ, std::max<uint64_t>(n, 1) * sizeof(ecdna_rep_summary_t)));
 
     c->row_stride = round_up(p->cell_cap, 64);
+    if (p->flags & ECDNA_FLAG_BIN_STORE) {
+        c->bin_k = p->bin_kmax ? p->bin_kmax : 64;
+        c->bin_c32 = p->cell_cap > 65535u ? 1 : 0;  // u16 counters hold at most 65535 cells per bin/group
+        c->stepper_block = (uint32_t)ecdna::bin_stepper_block(c->bin_k);
+    }
+    const uint64_t bag_bytes = (uint64_t)c->bin_k * (c->bin_c32 ? 4u : 2u);
     if (p->n_snapshots && n) {  // snapshot outputs cover the whole run (not chunked)
         CTX_TRY(hipMalloc(&c->d_snap_meta, n * p->n_snapshots * sizeof(ecdna_snapshot_t)));
         if (p->flags & ECDNA_FLAG_SNAPSHOT_ROWS)
@@ -329,7 +344,7 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
     }
 
     // rows: one u16 row per replicate of the chunk; chunk bounded by free HBM
-    const uint64_t row_bytes = c->row_stride * sizeof(uint16_t);
+    const uint64_t row_bytes = c->row_stride * sizeof(uint16_t) + bag_bytes;
     size_t free_b = 0, total_b = 0;
     CTX_TRY(hipMemGetInfo(&free_b, &total_b));
     uint64_t budget = (uint64_t)((double)free_b * 0.85);
@@ -340,7 +355,8 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
     if (max_chunk) fit = std::min<uint64_t>(fit, max_chunk);
     if (fit == 0) return bail(fail(ECDNA_E_NOMEM, "one replicate row does not fit in device memory"));
     c->chunk_reps = std::min<uint64_t>(std::max<uint64_t>(n, 1), fit);
-    CTX_TRY(hipMalloc(&c->d_rows, c->chunk_reps * row_bytes));
+    CTX_TRY(hipMalloc(&c->d_rows, c->chunk_reps * c->row_stride * sizeof(uint16_t)));
+    if (c->bin_k) CTX_TRY(hipMalloc(&c->d_bags, c->chunk_reps * bag_bytes));
 
     const uint64_t n_chunks = n ? (n + c->chunk_reps - 1) / c->chunk_reps : 0;
     CTX_TRY(hipMalloc(&c->d_heads, std::max<uint64_t>(n_chunks, 1) * sizeof(uint32_t)));
@@ -355,12 +371,19 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
     // persistent stepper grid: as many resident lanes as the occupancy allows
     c->window = env_u64("ECDNA_SSA_WINDOW", 1) ? 1 : 0;
     int per_cu = 0;
-    CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, ecdna::stepper_kernel(p->process, p->segregation, c->window), ecdna::kStepperBlock, 0));
-    // Memory-level parallelism of the random row accesses saturates HBM at about 3 resident 256-lane
-    // blocks per CU (C3 sweep, DESIGN.md §8: 1/2/3/4/7 blocks -> 617/372/329/336/349 ms); fewer
-    // lanes also mean more replicates per lane and a shorter drain once the work queue is empty.
-    per_cu = std::min(per_cu, 3);
+    if (c->bin_k) {
+        // bin store: LDS-resident events, bounded by issue and LDS latency: every resident block helps
+        CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, ecdna::bin_stepper_kernel(p->process, p->segregation, c->bin_k, c->bin_c32),
+            (int)c->stepper_block, 0));
+    } else {
+        CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, ecdna::stepper_kernel(p->process, p->segregation, c->window), ecdna::kStepperBlock, 0));
+        // Memory-level parallelism of the random row accesses saturates HBM at about 3 resident 256-lane
+        // blocks per CU (C3 sweep, DESIGN.md §8: 1/2/3/4/7 blocks -> 617/372/329/336/349 ms); fewer
+        // lanes also mean more replicates per lane and a shorter drain once the work queue is empty.
+        per_cu = std::min(per_cu, 3);
+    }
     uint64_t bpc = env_u64("ECDNA_SSA_BLOCKS_PER_CU", 0);
     if (bpc) per_cu = (int)bpc;
     if (per_cu < 1) per_cu = 1;
@@ -423,11 +446,15 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
         a.snap_cells = c->d_snap_cells;
         a.snap_meta = c->d_snap_meta ? c->d_snap_meta + ch.first * p.n_snapshots : nullptr;
         a.snap_rows = c->d_snap_rows ? c->d_snap_rows + ch.first * p.n_snapshots * c->row_stride : nullptr;
-        const uint32_t need = (ch.n + ecdna::kStepperBlock - 1) / ecdna::kStepperBlock;
+        a.bags = c->d_bags;
+        const uint32_t need = (ch.n + c->stepper_block - 1) / c->stepper_block;
         const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(need, c->stepper_blocks_cap));
 
         HIP_TRY(hipEventRecord(ch.ev[0], st));
-        HIP_TRY(ecdna::launch_stepper(a, p.process, p.segregation, c->window, blocks, st));
+        if (c->bin_k)
+            HIP_TRY(ecdna::launch_bin_stepper(a, p.process, p.segregation, c->bin_k, c->bin_c32, blocks, st));
+        else
+            HIP_TRY(ecdna::launch_stepper(a, p.process, p.segregation, c->window, blocks, st));
         HIP_TRY(hipEventRecord(ch.ev[1], st));
 
         ecdna::HistArgs hsa{};
@@ -450,6 +477,9 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
         hsa.target_entropy = c->target_entropy;
         hsa.target_freq = c->target_freq;
         hsa.has_target = c->has_target ? 1u : 0u;
+        hsa.bags = c->d_bags;
+        hsa.bag_k = c->bin_k;
+        hsa.bag_c32 = (uint32_t)c->bin_c32;
         const uint32_t hblocks = (ch.n + rpb - 1) / rpb;
         HIP_TRY(ecdna::launch_hist(hsa, hblocks, st));
         HIP_TRY(hipEventRecord(ch.ev[2], st));
@@ -492,7 +522,7 @@ int64_t ecdna_ssa_ctx_row_stride(const ecdna_ssa_ctx* c) {
 int ecdna_ssa_ctx_geometry(const ecdna_ssa_ctx* c, uint64_t* chunk_replicates, uint64_t* grid_lanes) {
     if (!c) return fail(ECDNA_E_INVALID, "ctx is NULL");
     if (chunk_replicates) *chunk_replicates = c->chunk_reps;
-    if (grid_lanes) *grid_lanes = (uint64_t)c->stepper_blocks_cap * ecdna::kStepperBlock;
+    if (grid_lanes) *grid_lanes = (uint64_t)c->stepper_blocks_cap * c->stepper_block;
     return ECDNA_OK;
 }
 
@@ -516,6 +546,33 @@ int ecdna_ssa_ctx_download(ecdna_ssa_ctx* c, ecdna_rep_summary_t* out_summaries,
         if (p.n_replicates)
             HIP_TRY(hipMemcpy(out_rows, c->d_rows, p.n_replicates * c->row_stride * sizeof(uint16_t),
                               hipMemcpyDeviceToHost));
+        if (c->bin_k && p.n_replicates) {
+            // bin store: canonical rows = the counters expanded (k ascending), then the large-k row
+            std::vector<ecdna_rep_summary_t> summ(p.n_replicates);
+            HIP_TRY(hipMemcpy(summ.data(), c->d_summ, p.n_replicates * sizeof(ecdna_rep_summary_t),
+                              hipMemcpyDeviceToHost));
+            const uint64_t kb = c->bin_k;
+            std::vector<uint32_t> bags(p.n_replicates * kb);
+            if (c->bin_c32) {
+                HIP_TRY(hipMemcpy(bags.data(), c->d_bags, bags.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+            } else {
+                std::vector<uint16_t> b16(bags.size());
+                HIP_TRY(hipMemcpy(b16.data(), c->d_bags, b16.size() * sizeof(uint16_t), hipMemcpyDeviceToHost));
+                std::copy(b16.begin(), b16.end(), bags.begin());
+            }
+            std::vector<uint16_t> big;
+            for (uint64_t i = 0; i < p.n_replicates; ++i) {
+                uint16_t* r = out_rows + i * c->row_stride;
+                uint64_t small = 0;
+                for (uint64_t b = 0; b < kb; ++b) small += bags[i * kb + b];
+                const uint64_t nbig = summ[i].nplus >= small ? summ[i].nplus - small : 0;
+                big.assign(r, r + nbig);
+                uint64_t pos = 0;
+                for (uint64_t b = 0; b < kb; ++b)
+                    for (uint32_t q = 0; q < bags[i * kb + b]; ++q) r[pos++] = (uint16_t)(b + 1);
+                std::copy(big.begin(), big.end(), r + pos);
+            }
+        }
     }
     return ECDNA_OK;
 }

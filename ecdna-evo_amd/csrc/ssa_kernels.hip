@@ -369,6 +369,388 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
     }
 }
 
+// ---------------------------------------------------------------- bin store (ECDNA_FLAG_BIN_STORE)
+//
+// DESIGN.md §3.3 / §5. A lane's N+ cells are counts c[k] of cells with k copies, k = 1..K with
+// K = 8 * NG, held in LDS, plus a row B (HBM, the replicate's row) of the cells with k > K. The uniform
+// cell pick indexes the canonical order (all k = 1 cells, then k = 2, ..., then B), found by a two-level
+// scan: NG group sums (8 bins each), then the 8 bins of the chosen group. Each is one or two 16-B LDS
+// reads per lane; updates are fire-and-forget LDS atomic adds on the packed counters. In the common case
+// (every copy number involved <= K) an event touches no HBM at all.
+//
+// LDS per lane: counts NG*8 (u16, or u32 when C32) + NG group sums of the same width, laid out
+// [vector][lane] in 16-B vectors so a wave's 16-B reads are contiguous (conflict-free).
+template <int NG, bool C32>
+struct BinLayout {
+    static constexpr int kK = 8 * NG;                       // binned copy numbers 1..kK
+    static constexpr int kPerVec = C32 ? 4 : 8;             // counters per 16-B vector
+    static constexpr int kGroupVecs = 8 / kPerVec;          // vectors per group of 8 bins
+    static constexpr int kBinVecs = NG * kGroupVecs;
+    static constexpr int kSumVecs = (NG + kPerVec - 1) / kPerVec;
+};
+
+// Counter j of a 16-B vector (8 x u16 or 4 x u32)
+template <bool C32>
+__device__ __forceinline__ uint32_t vec_get(const uint4& v, int j) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    if (C32) return w[j];
+    return (w[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
+}
+
+template <bool BD, int SEG, int NG, bool C32, int BLK>
+__global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
+    using L = BinLayout<NG, C32>;
+    constexpr uint32_t K = L::kK;
+    __shared__ uint4 cnt_v[L::kBinVecs][BLK];  // bin counters
+    __shared__ uint4 sum_v[L::kSumVecs][BLK];  // group sums
+    const uint32_t tid = threadIdx.x;
+    const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+    const bool f32t = (a.flags & ECDNA_FLAG_TIME_F32) != 0;
+    const bool hash_on = (a.flags & ECDNA_FLAG_EVENT_HASH) != 0;
+
+    // packed counter add: bin b (0-based, copy number b + 1) / group g, by +1 or -1 (two's complement
+    // on the 32-bit word: a 16-bit field never borrows from its neighbour because it is >= 1 when
+    // decremented)
+    auto word_of_bin = [&](uint32_t b) -> uint32_t* {
+        const uint32_t v = C32 ? (b >> 2) : (b >> 3);
+        const uint32_t w = C32 ? (b & 3u) : ((b & 7u) >> 1);
+        return reinterpret_cast<uint32_t*>(&cnt_v[v][tid]) + w;
+    };
+    auto word_of_group = [&](uint32_t g) -> uint32_t* {
+        const uint32_t v = C32 ? (g >> 2) : (g >> 3);
+        const uint32_t w = C32 ? (g & 3u) : ((g & 7u) >> 1);
+        return reinterpret_cast<uint32_t*>(&sum_v[v][tid]) + w;
+    };
+    auto unit = [&](uint32_t idx) -> uint32_t { return C32 ? 1u : (1u << ((idx & 1u) * 16)); };
+    auto bin_add = [&](uint32_t k, bool inc) {  // k in 1..K
+        const uint32_t b = k - 1, g = b >> 3;
+        const uint32_t ub = unit(b), ug = unit(g);
+        atomicAdd(word_of_bin(b), inc ? ub : 0u - ub);
+        atomicAdd(word_of_group(g), inc ? ug : 0u - ug);
+    };
+    // canonical position i < ns -> copy number
+    auto bin_find = [&](uint32_t i) -> uint32_t {
+        uint32_t run = 0, g = 0, base = 0;
+#pragma unroll
+        for (int v = 0; v < L::kSumVecs; ++v) {
+            const uint4 sv = sum_v[v][tid];
+#pragma unroll
+            for (int j = 0; j < L::kPerVec; ++j) {
+                if (v * L::kPerVec + j >= NG) break;
+                run += vec_get<C32>(sv, j);
+                const bool le = run <= i;
+                g += le ? 1u : 0u;
+                base = le ? run : base;
+            }
+        }
+        const uint32_t r = i - base;
+        uint32_t run2 = 0, b = 0;
+#pragma unroll
+        for (int v = 0; v < L::kGroupVecs; ++v) {
+            const uint4 cv = cnt_v[g * L::kGroupVecs + v][tid];
+#pragma unroll
+            for (int j = 0; j < L::kPerVec; ++j) {
+                run2 += vec_get<C32>(cv, j);
+                b += (run2 <= r) ? 1u : 0u;
+            }
+        }
+        return g * 8u + b + 1u;
+    };
+    auto bins_zero = [&]() {
+#pragma unroll
+        for (int v = 0; v < L::kBinVecs; ++v) cnt_v[v][tid] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int v = 0; v < L::kSumVecs; ++v) sum_v[v][tid] = make_uint4(0, 0, 0, 0);
+    };
+    // canonical row (bins ascending, then B) -> dst; B lives at row[0, nb)
+    auto expand = [&](uint16_t* dst, const uint16_t* big, uint32_t nb) {  // rare path: keep it a plain loop
+        uint32_t pos = 0;
+#pragma unroll 1
+        for (uint32_t b = 0; b < K; ++b) {
+            const uint32_t c = C32 ? *word_of_bin(b) : ((*word_of_bin(b) >> ((b & 1u) * 16)) & 0xffffu);
+#pragma unroll 1
+            for (uint32_t q = 0; q < c; ++q) dst[pos++] = (uint16_t)(b + 1u);
+        }
+#pragma unroll 1
+        for (uint32_t j = 0; j < nb; ++j) dst[pos + j] = big[j];
+    };
+
+    bool active = false, have = false;
+    uint32_t li = 0;
+    uint64_t rid = 0;
+    uint16_t* row = a.rows;
+    uint32_t nm = 0, ns = 0, nb = 0;
+    float b0 = 0.f, b1 = 0.f, d0 = 0.f, d1 = 0.f;
+    double t = 0.0;
+    float t32 = 0.f;
+    uint32_t e = 0, n_pm = 0, n_pp = 0, n_dm = 0, n_dp = 0, n_un = 0;
+    uint64_t h = kFnvOffset;
+    uint32_t stop = 0, err = 0;
+    uint32_t sj = 0;
+
+    for (;;) {
+        if (!active) {
+            if (have) {
+                // final bin counters -> bags[li] (B stays in the row)
+                uint4* bag = reinterpret_cast<uint4*>(a.bags) + (uint64_t)li * L::kBinVecs;
+#pragma unroll
+                for (int v = 0; v < L::kBinVecs; ++v) bag[v] = cnt_v[v][tid];
+                ecdna_rep_summary_t* s = a.summaries + li;
+                s->nminus = nm;
+                s->nplus = ns + nb;
+                s->iters = e;
+                s->events_by_type[0] = n_pm;
+                s->events_by_type[1] = n_pp;
+                s->events_by_type[2] = n_dm;
+                s->events_by_type[3] = n_dp;
+                s->uneven = n_un;
+                s->time = f32t ? (double)t32 : t;
+                s->event_hash = hash_on ? h : 0ull;
+                s->stop_reason = stop;
+                s->error = err;
+            }
+            const uint32_t i = atomicAdd(a.head, 1u);
+            if (i >= a.n) break;
+            have = true;
+            active = true;
+            li = i;
+            rid = a.rid0 + i;
+            row = a.rows + (uint64_t)i * a.row_stride;
+            const uint64_t set = rid / a.reps_per_set;
+            const float4 r = a.rates[set];
+            b0 = r.x;
+            b1 = r.y;
+            d0 = r.z;
+            d1 = r.w;
+            const uint16_t* src = a.init_copies;
+            uint32_t cnt = a.init_nplus;
+            if (a.init_offsets) {
+                src = a.init_copies + a.init_offsets[set];
+                cnt = a.init_offsets[set + 1] - a.init_offsets[set];
+            }
+            bins_zero();
+            ns = 0;
+            nb = 0;
+            for (uint32_t j = 0; j < cnt; ++j) {
+                const uint32_t kk = src[j];
+                if (kk <= K) {
+                    bin_add(kk, true);
+                    ++ns;
+                } else {
+                    row[nb++] = (uint16_t)kk;
+                }
+            }
+            nm = (uint32_t)(a.init_nminus_set ? a.init_nminus_set[set] : a.init_nminus);
+            t = 0.0;
+            t32 = 0.f;
+            e = n_pm = n_pp = n_dm = n_dp = n_un = 0;
+            h = kFnvOffset;
+            stop = 0;
+            err = 0;
+            sj = 0;
+            if (ns + nb == 0 && nm == 0) {  // ensure!(!distribution.is_empty()) src/process.rs:88, 232
+                err = ECDNA_REP_ERR_EMPTY;
+                stop = ECDNA_STOP_ERROR;
+                active = false;
+                continue;
+            }
+        }
+        const uint32_t np = ns + nb;
+
+        // propensities rate_i * population_i over [n-, n+(, n-, n+)]
+        const double pa = (double)b0 * (double)nm;
+        const double pb = (double)b1 * (double)np;
+        const double cA = pa;
+        const double cB = cA + pb;
+        double cC = cB, a0 = cB;
+        if (BD) {
+            const double pc = (double)d0 * (double)nm;
+            const double pd = (double)d1 * (double)np;
+            cC = cB + pc;
+            a0 = cC + pd;
+        }
+        {
+            const bool t_over = f32t ? (t32 >= a.max_time32) : (t >= a.max_time);
+            uint32_t s = (a0 > 0.0) ? 0u : (uint32_t)ECDNA_STOP_ABSORBING;
+            s = t_over ? (uint32_t)ECDNA_STOP_MAX_TIME : s;
+            s = ((uint64_t)nm + np >= a.stop_cells) ? (uint32_t)ECDNA_STOP_MAX_CELLS : s;
+            s = (e >= a.max_iter) ? (uint32_t)ECDNA_STOP_MAX_ITER : s;
+            if (s) {
+                stop = s;
+                active = false;
+                continue;
+            }
+        }
+        if (a.n_snap) {  // src/process.rs:122-145, as in ssa_stepper
+            const uint64_t total = (uint64_t)nm + np;
+            while (sj < a.n_snap) {
+                bool any = false;
+                for (uint32_t q = 0; q < a.n_snap; ++q) any |= (q >= sj) && (a.snap_cells[q] == total);
+                if (!any) break;
+                ecdna_snapshot_t* m = a.snap_meta + (uint64_t)li * a.n_snap + sj;
+                m->time = f32t ? (double)t32 : t;
+                m->nminus = nm;
+                m->nplus = np;
+                m->taken = 1u;
+                m->reserved = 0u;
+                if (a.snap_rows) expand(a.snap_rows + ((uint64_t)li * a.n_snap + sj) * a.row_stride, row, nb);
+                ++sj;
+            }
+        }
+
+        const uint32_t rid_lo = (uint32_t)rid, rid_hi = (uint32_t)(rid >> 32);
+        const uint4 w = philox4x32_10(make_uint4(e, 0u, rid_lo, rid_hi), k0, k1);
+        const double target = (((double)w.y + 0.5) * 0x1p-32) * a0;
+        uint32_t ch;
+        if (BD)
+            ch = target < cA ? 0u : (target < cB ? 1u : (target < cC ? 2u : 3u));
+        else
+            ch = target < cA ? 0u : 1u;
+
+        WordStream ws;
+        ws.w2 = w.z;
+        ws.w3 = w.w;
+        ws.e = e;
+        ws.rid_lo = rid_lo;
+        ws.rid_hi = rid_hi;
+        ws.k0 = k0;
+        ws.k1 = k1;
+        ws.pos = 1;
+        ws.blk_id = 0;
+        ws.blk = make_uint4(0, 0, 0, 0);
+
+        uint32_t idx = 0, k = 0;
+        bool small = true;
+        if (ch & 1u) {
+            uint64_t m = (uint64_t)w.z * np;
+            uint32_t lo = (uint32_t)m;
+            if (lo < np) {
+                const uint32_t thr = (0u - np) % np;
+                while (lo < thr) {
+                    m = (uint64_t)ws.next() * np;
+                    lo = (uint32_t)m;
+                }
+            }
+            idx = (uint32_t)(m >> 32);
+            small = idx < ns;
+            if (small)
+                k = bin_find(idx);
+            else
+                k = gload_u16(row + (idx - ns));
+        }
+
+        uint32_t n = 0, k1v = 0;
+        uint32_t un = 0;
+        if (ch == 1u) {
+            if (k > 32767u) {  // checked_mul panic (src/proliferation.rs:63-67)
+                err = ECDNA_REP_ERR_OVERFLOW;
+                stop = ECDNA_STOP_ERROR;
+                active = false;
+                continue;
+            }
+            n = 2u * k;
+            if (SEG == ECDNA_SEG_DETERMINISTIC) {
+                k1v = k;
+            } else {
+                if (ws.pos == 1 && n <= 32u) {
+                    k1v = __popc(n == 32u ? w.w : (w.w & ((1u << n) - 1u)));
+                    ws.pos = 2;
+                } else {
+                    k1v = ws.binomial_half(n);
+                }
+                if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN) {
+                    uint32_t tries = 1;
+                    bool rej = false;
+                    while (k1v == 0u || k1v == n) {
+                        if (tries == kNoUnevenMaxTries) {
+                            rej = true;
+                            break;
+                        }
+                        k1v = ws.binomial_half(n);
+                        ++tries;
+                    }
+                    if (rej) {
+                        err = ECDNA_REP_ERR_REJECTION;
+                        stop = ECDNA_STOP_ERROR;
+                        active = false;
+                        continue;
+                    }
+                } else if (k1v == 0u || k1v == n) {
+                    un = (SEG == ECDNA_SEG_BINOMIAL_NO_NMINUS) ? 2u : 1u;
+                }
+            }
+            if (un == 0u && np + 1u > a.cell_cap) {
+                err = ECDNA_REP_ERR_CELL_CAP;
+                stop = ECDNA_STOP_ERROR;
+                active = false;
+                continue;
+            }
+        }
+
+        const double tau = softlog_neg(w.x) / a0;
+
+        uint64_t x = ch;
+        if (ch & 1u) {
+            // daughters (none for a death): [k1, k2] on an even split, [n] on an uneven one
+            const bool prolif = ch == 1u;
+            const uint32_t da = (un == 0u) ? k1v : n;
+            const uint32_t db = n - k1v;
+            const bool has_a = prolif, has_b = prolif && un == 0u;
+            if (small) {
+                bin_add(k, false);
+                ns -= 1;
+            }
+            uint32_t open = small ? 0xffffffffu : idx - ns;  // B slot freed by a large picked cell
+            if (has_a) {
+                if (da <= K) {
+                    bin_add(da, true);
+                    ns += 1;
+                } else if (open != 0xffffffffu) {
+                    row[open] = (uint16_t)da;
+                    open = 0xffffffffu;
+                } else {
+                    row[nb++] = (uint16_t)da;
+                }
+            }
+            if (has_b) {
+                if (db <= K) {
+                    bin_add(db, true);
+                    ns += 1;
+                } else if (open != 0xffffffffu) {
+                    row[open] = (uint16_t)db;
+                    open = 0xffffffffu;
+                } else {
+                    row[nb++] = (uint16_t)db;
+                }
+            }
+            if (open != 0xffffffffu) {  // swap_remove(open) from B
+                if (open != nb - 1) row[open] = (uint16_t)gload_u16(row + nb - 1);
+                nb -= 1;
+            }
+            if (prolif) {
+                if (un != 0u) {
+                    nm += (un == 1u) ? 1u : 0u;
+                    n_un += 1;
+                }
+                x |= ((uint64_t)k1v << 2) | ((uint64_t)idx << 20);
+            } else {
+                x |= (uint64_t)idx << 20;
+            }
+        }
+        nm = nm + (ch == 0u ? 1u : 0u) - ((BD && ch == 2u) ? 1u : 0u);
+        n_pm += ch == 0u ? 1u : 0u;
+        n_pp += ch == 1u ? 1u : 0u;
+        n_dm += ch == 2u ? 1u : 0u;
+        n_dp += ch == 3u ? 1u : 0u;
+        e += 1;
+        if (f32t)
+            t32 = t32 + (float)tau;
+        else
+            t = t + tau;
+        if (hash_on) h = (h ^ x) * kFnvPrime;
+    }
+}
+
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS accesses have completed
     __builtin_amdgcn_wave_barrier();
@@ -393,7 +775,9 @@ __device__ __forceinline__ double wave_max(double x) {
 // STATS: each wave first builds its replicate's own histogram in LDS (u32 per bin), derives the
 // replicate's ABC statistics from it (mean, entropy, N+ frequency, KS distance to the target CDF by
 // a wave prefix scan over the bins — abc.md:38-55), then adds it to the workgroup histogram.
-template <bool STATS>
+// BAG (bin store, ECDNA_FLAG_BIN_STORE): 0 = rows only; 1 / 2 = per-replicate u16 / u32 bin counters
+// bags[q][bag_k] for copy numbers 1..bag_k, plus the large-k cells at the head of the row.
+template <bool STATS, int BAG>
 __global__ void __launch_bounds__(kHistBlock) ssa_hist(const HistArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds[];
     unsigned long long* hb = lds;                // [bins]
@@ -422,12 +806,32 @@ __global__ void __launch_bounds__(kHistBlock) ssa_hist(const HistArgs a) {
                 wave_sync_lds();
             }
             uint64_t ksum = 0;
-            for (uint32_t c = lane * 8u; c < np; c += 512u) {
+            uint32_t nrow = np;  // cells held in the row
+            if (BAG) {
+                uint32_t small = 0;
+                for (uint32_t b = lane; b < a.bag_k; b += 64u) {
+                    const uint64_t o = (uint64_t)q * a.bag_k + b;
+                    const uint32_t cnt = BAG == 2 ? reinterpret_cast<const uint32_t*>(a.bags)[o]
+                                                  : (uint32_t)reinterpret_cast<const uint16_t*>(a.bags)[o];
+                    if (cnt) {
+                        const uint32_t kk = b + 1u;
+                        if (STATS) {
+                            atomicAdd(&wh[kk < last ? kk : last], cnt);
+                            ksum += (uint64_t)kk * cnt;
+                        } else {
+                            atomicAdd(&hb[kk < last ? kk : last], (unsigned long long)cnt);
+                        }
+                    }
+                    small += cnt;
+                }
+                nrow = np - wave_sum(small);
+            }
+            for (uint32_t c = lane * 8u; c < nrow; c += 512u) {
                 const uint4 v = *reinterpret_cast<const uint4*>(row + c);
                 const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    if (c + (uint32_t)j < np) {
+                    if (c + (uint32_t)j < nrow) {
                         const uint32_t kk = (wv[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
                         if (STATS) {
                             atomicAdd(&wh[kk < last ? kk : last], 1u);
@@ -510,9 +914,27 @@ static const void* const kStepperTable[2][2][4] = {
     {ECDNA_STEPPER_TABLE(false, false), ECDNA_STEPPER_TABLE(true, false)},
     {ECDNA_STEPPER_TABLE(false, true), ECDNA_STEPPER_TABLE(true, true)}};
 
+// bin-store variants: [birth_death][segregation][K = 64 | 256][u16 | u32 counters]; the 256-bin
+// u32 variant runs 64-lane blocks (its 72 KiB of LDS per 64 lanes)
+#define ECDNA_BIN_SEG(BD, SEG)                                                                             \
+    {{(const void*)ssa_stepper_bins<BD, SEG, 8, false, kStepperBlock>,                                      \
+      (const void*)ssa_stepper_bins<BD, SEG, 8, true, kStepperBlock>},                                      \
+     {(const void*)ssa_stepper_bins<BD, SEG, 32, false, kBinWideBlock>,                                     \
+      (const void*)ssa_stepper_bins<BD, SEG, 32, true, kBinWideBlock>}}
+#define ECDNA_BIN_TABLE(BD) \
+    {ECDNA_BIN_SEG(BD, 0), ECDNA_BIN_SEG(BD, 1), ECDNA_BIN_SEG(BD, 2), ECDNA_BIN_SEG(BD, 3)}
+
+static const void* const kBinStepperTable[2][4][2][2] = {ECDNA_BIN_TABLE(false), ECDNA_BIN_TABLE(true)};
+
 const void* stepper_kernel(int birth_death, int segregation, int window) {
     return kStepperTable[window ? 1 : 0][birth_death ? 1 : 0][segregation & 3];
 }
+
+const void* bin_stepper_kernel(int birth_death, int segregation, uint32_t bin_k, int c32) {
+    return kBinStepperTable[birth_death ? 1 : 0][segregation & 3][bin_k > 64 ? 1 : 0][c32 ? 1 : 0];
+}
+
+int bin_stepper_block(uint32_t bin_k) { return bin_k > 64 ? kBinWideBlock : kStepperBlock; }
 
 hipError_t launch_stepper(const StepperArgs& a, int birth_death, int segregation, int window, uint32_t blocks,
                           hipStream_t stream) {
@@ -522,13 +944,24 @@ hipError_t launch_stepper(const StepperArgs& a, int birth_death, int segregation
                            0, stream);
 }
 
+hipError_t launch_bin_stepper(const StepperArgs& a, int birth_death, int segregation, uint32_t bin_k, int c32,
+                              uint32_t blocks, hipStream_t stream) {
+    StepperArgs copy = a;
+    void* args[] = {&copy};
+    return hipLaunchKernel(bin_stepper_kernel(birth_death, segregation, bin_k, c32), dim3(blocks),
+                           dim3(bin_stepper_block(bin_k)), args, 0, stream);
+}
+
 hipError_t launch_hist(const HistArgs& a, uint32_t blocks, hipStream_t stream) {
     HistArgs copy = a;
     void* args[] = {&copy};
     size_t lds = (size_t)(a.bins + 16) * sizeof(unsigned long long);
     if (a.stats) lds += (size_t)(kHistBlock / 64) * a.bins * sizeof(uint32_t);  // per-wave replicate histograms
-    const void* k = a.stats ? (const void*)ssa_hist<true> : (const void*)ssa_hist<false>;
-    return hipLaunchKernel(k, dim3(blocks), dim3(kHistBlock), args, lds, stream);
+    static const void* const table[2][3] = {
+        {(const void*)ssa_hist<false, 0>, (const void*)ssa_hist<false, 1>, (const void*)ssa_hist<false, 2>},
+        {(const void*)ssa_hist<true, 0>, (const void*)ssa_hist<true, 1>, (const void*)ssa_hist<true, 2>}};
+    const int bag = a.bags ? (a.bag_c32 ? 2 : 1) : 0;
+    return hipLaunchKernel(table[a.stats ? 1 : 0][bag], dim3(blocks), dim3(kHistBlock), args, lds, stream);
 }
 
 }  // namespace ecdna

@@ -37,6 +37,7 @@ struct StepperArgs {
     const uint64_t* snap_cells;     // [n_snap], ascending
     ecdna_snapshot_t* snap_meta;    // [n][n_snap], chunk-offset
     uint16_t* snap_rows;            // [n][n_snap][row_stride] or nullptr, chunk-offset
+    void* bags;                     // bin store: [n][bin_k] final u16 / u32 bin counters (chunk-local)
 };
 
 // Histogram / totals pass over one chunk.
@@ -56,9 +57,14 @@ struct HistArgs {
     const double* target_cdf;
     double target_mean, target_entropy, target_freq;
     uint32_t has_target;
+    // bin store: per-replicate counters [n][bag_k] (u16, or u32 when bag_c32); nullptr = rows only
+    const void* bags;
+    uint32_t bag_k;
+    uint32_t bag_c32;
 };
 
 constexpr int kStepperBlock = 256;
+constexpr int kBinWideBlock = 64;  // bin store with 256 bins
 constexpr int kHistBlock = 256;
 constexpr uint32_t kMaxHistBins = 4096;  // LDS: 8 B per bin per workgroup (<= 64 KiB)
 constexpr uint32_t kMaxSnapshots = 64;
@@ -68,6 +74,12 @@ constexpr uint32_t kMaxSnapshots = 64;
 const void* stepper_kernel(int birth_death, int segregation, int window);
 hipError_t launch_stepper(const StepperArgs& a, int birth_death, int segregation, int window, uint32_t blocks,
                           hipStream_t stream);
+// Bin store (ECDNA_FLAG_BIN_STORE): bin_k = 64 or 256 binned copy numbers; c32 = u32 counters
+// (cell_cap > 65535). bin_stepper_block = the variant's workgroup size.
+const void* bin_stepper_kernel(int birth_death, int segregation, uint32_t bin_k, int c32);
+int bin_stepper_block(uint32_t bin_k);
+hipError_t launch_bin_stepper(const StepperArgs& a, int birth_death, int segregation, uint32_t bin_k, int c32,
+                              uint32_t blocks, hipStream_t stream);
 hipError_t launch_hist(const HistArgs& a, uint32_t blocks, hipStream_t stream);
 
 }  // namespace ecdna

@@ -14,7 +14,7 @@ from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # ecdna_process_t (ProcessType, src/clap_app.rs:311-315)
 PURE_BIRTH = 0
@@ -76,7 +76,7 @@ class Params(C.Structure):
         ("flags", C.c_uint32),
         ("init_copies", C.POINTER(C.c_uint16)),
         ("init_nplus", C.c_uint32),
-        ("reserved0", C.c_uint32),
+        ("bin_kmax", C.c_uint32),
         ("init_nminus", C.c_uint64),
         ("init_set_offsets", C.POINTER(C.c_uint32)),
         ("init_set_nminus", C.POINTER(C.c_uint64)),
@@ -93,6 +93,7 @@ STATS_DTYPE = np.dtype([("mean", "<f8"), ("entropy", "<f8"), ("frequency", "<f8"
                         ("mean_rel", "<f8"), ("entropy_rel", "<f8"), ("frequency_diff", "<f8"), ("cells", "<u8")])
 assert STATS_DTYPE.itemsize == 64
 FLAG_REP_STATS = 0x10
+FLAG_BIN_STORE = 0x20  # cells binned by copy number; bin_kmax = 64 or 256
 
 
 SNAPSHOT_DTYPE = np.dtype([("time", "<f8"), ("nminus", "<u8"), ("nplus", "<u8"), ("taken", "<u4"),
@@ -168,6 +169,7 @@ class RunSpec:
     device: int = 0
     snapshots: Optional[Sequence[int]] = None  # cell counts (sorted here); None = no snapshots
     stats_target: Optional[Sequence[int]] = None  # target histogram [hist_bins] for ABC distances
+    bin_kmax: int = 0  # FLAG_BIN_STORE: binned copy numbers 1..bin_kmax (0 = 64)
     _keep: list = field(default_factory=list, repr=False)
 
     def resolved_max_time(self) -> float:
@@ -212,6 +214,7 @@ class RunSpec:
         p.max_time = self.resolved_max_time()
         p.max_iter = self.max_iter
         p.flags = self.flags
+        p.bin_kmax = self.bin_kmax
         p.device = self.device
         if self.snapshots:
             snaps = np.asarray(sorted(int(x) for x in self.snapshots), dtype=np.uint64)

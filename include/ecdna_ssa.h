@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ECDNA_SSA_ABI_VERSION 3
+#define ECDNA_SSA_ABI_VERSION 4
 
 /* Process type — ProcessType (src/clap_app.rs:311-315); chosen as BirthDeath
  * when d0 > 0 or d1 > 0 (src/clap_app.rs:163-174, 194-200). */
@@ -97,6 +97,15 @@ typedef enum {
 #define ECDNA_FLAG_EVENT_HASH 0x4u     /* fold every event into ecdna_rep_summary_t.event_hash */
 #define ECDNA_FLAG_SNAPSHOT_ROWS 0x8u  /* keep the N+ row of every snapshot (else only its metadata) */
 #define ECDNA_FLAG_REP_STATS 0x10u     /* per-replicate ABC statistics (ecdna_rep_stats_t) */
+/* Cell store of a replicate's N+ cells. Default: the ROW store, one u16 per cell
+ * in the reference's swap_remove order (ecdna-lib EcDNADistribution.nplus: Vec<u16>). With this flag:
+ * the BIN store, per-replicate counts of cells by copy number k = 1..bin_kmax held in LDS, plus a
+ * row of the cells with k > bin_kmax. A uniform cell pick has the same law under any arrangement
+ * of the cells, so both stores simulate the same process; they consume the same draws but address
+ * cells in a different order, so their runs differ seed for seed (each is bit-exact with its own
+ * oracle restatement). Final and snapshot rows come back in canonical order: k = 1 cells, k = 2
+ * cells, ..., k = bin_kmax cells, then the large-k row. */
+#define ECDNA_FLAG_BIN_STORE 0x20u
 
 /* API return codes. */
 #define ECDNA_OK 0
@@ -137,7 +146,8 @@ typedef struct {
      * into init_copies, init_set_nminus[n_param_sets]). Copy numbers must be >= 1. */
     const uint16_t* init_copies;    /* host */
     uint32_t init_nplus;
-    uint32_t reserved0;
+    uint32_t bin_kmax;              /* ECDNA_FLAG_BIN_STORE: copy numbers 1..bin_kmax are binned; 64 or 256
+                                       (0 = 64); part of the draw mapping (the canonical cell order) */
     uint64_t init_nminus;
     const uint32_t* init_set_offsets; /* host or NULL */
     const uint64_t* init_set_nminus;  /* host or NULL */
@@ -236,12 +246,14 @@ int ecdna_ssa_ctx_sync(ecdna_ssa_ctx* c, float* ssa_ms, float* hist_ms);
 int ecdna_ssa_ctx_device_outputs(ecdna_ssa_ctx* c, uint64_t** d_hist, ecdna_totals_t** d_totals);
 /* Copy results of the last launch to HOST buffers (each may be NULL). out_rows, if given, receives
  * [n_replicates][row_stride] u16 where row i holds the final N+ copies of replicate i in the
- * engine's swap_remove order (entries past summaries[i].nplus are unspecified). Valid only when the
+ * engine's swap_remove order (row store) or in canonical order (bin store, ECDNA_FLAG_BIN_STORE);
+ * entries past summaries[i].nplus are unspecified. Valid only when the
  * whole run fit in one chunk (ecdna_ssa_ctx_row_stride returns > 0). */
 int ecdna_ssa_ctx_download(ecdna_ssa_ctx* c, ecdna_rep_summary_t* out_summaries, uint64_t* out_hist,
                            ecdna_totals_t* out_totals, uint16_t* out_rows);
 /* Snapshots of the last launch: meta[n_replicates][n_snapshots] and, under ECDNA_FLAG_SNAPSHOT_ROWS,
- * rows[n_replicates][n_snapshots][row_stride] u16 (the N+ cells in swap_remove order at the save).
+ * rows[n_replicates][n_snapshots][row_stride] u16 (the N+ cells at the save, in the order of
+ * ecdna_ssa_ctx_download).
  * Either may be NULL. */
 int ecdna_ssa_ctx_download_snapshots(ecdna_ssa_ctx* c, ecdna_snapshot_t* meta, uint16_t* rows);
 /* Per-replicate statistics of the last launch (needs ECDNA_FLAG_REP_STATS): out[n_replicates]. */

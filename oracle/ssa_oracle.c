@@ -258,6 +258,115 @@ static uint32_t death_nplus(uint16_t* row, uint64_t* len, wstream* ws) {
     return i;
 }
 
+/* ------------------------------------------------------------ bin store */
+
+/* The engine's BIN store (ECDNA_FLAG_BIN_STORE): the replicate's N+ cells as counts
+ * c[k] of cells with k copies for k = 1..K (K = bin_kmax), plus a row B of the cells with k > K.
+ * Canonical order of the N+ cells: c[1] cells of k = 1, c[2] of k = 2, ..., c[K] of k = K, then
+ * B[0..nb). The uniform pick (gen_range over the cells, src/proliferation.rs:57, 132) indexes that
+ * order; any fixed arrangement gives the same law, so this stands in for the Vec<u16> with
+ * swap_remove of ecdna-lib 3.0.2 in distribution, not seed for seed. */
+#define BIN_KMAX_MAX 256
+typedef struct {
+    uint32_t K;
+    uint64_t c[BIN_KMAX_MAX + 1]; /* c[1..K] */
+    uint64_t ns;                  /* sum of c */
+    uint16_t* big;                /* B */
+    uint64_t nb;
+} binstore;
+
+static void bins_add(binstore* b, uint32_t k) {
+    if (k <= b->K) {
+        b->c[k] += 1;
+        b->ns += 1;
+    } else {
+        b->big[b->nb++] = (uint16_t)k;
+    }
+}
+
+/* copy number of the cell at canonical position idx < ns + nb */
+static uint32_t bins_get(const binstore* b, uint64_t idx) {
+    if (idx >= b->ns) return b->big[idx - b->ns];
+    uint64_t run = 0;
+    for (uint32_t k = 1;; ++k) {
+        run += b->c[k];
+        if (idx < run) return k;
+    }
+}
+
+/* Remove the picked cell (canonical position idx, copy number k) and add the daughters d[0..nd):
+ * daughters with k <= K go to their bins; large ones: if the removed cell was itself in B (at j),
+ * the first large daughter takes its slot j and the rest are pushed; otherwise they are all pushed
+ * in order. A removed B cell with no large daughter is swap_removed from B. */
+static void bins_replace(binstore* b, uint64_t idx, uint32_t k, const uint32_t* d, int nd) {
+    int slot_open = 0;
+    uint64_t j = 0;
+    if (idx < b->ns) {
+        b->c[k] -= 1;
+        b->ns -= 1;
+    } else {
+        slot_open = 1;
+        j = idx - b->ns;
+    }
+    for (int q = 0; q < nd; ++q) {
+        if (d[q] <= b->K) {
+            b->c[d[q]] += 1;
+            b->ns += 1;
+        } else if (slot_open) {
+            b->big[j] = (uint16_t)d[q];
+            slot_open = 0;
+        } else {
+            b->big[b->nb++] = (uint16_t)d[q];
+        }
+    }
+    if (slot_open) { /* swap_remove(j) */
+        b->big[j] = b->big[b->nb - 1];
+        b->nb -= 1;
+    }
+}
+
+/* canonical row of the N+ cells */
+static void bins_expand(const binstore* b, uint16_t* dst) {
+    uint64_t pos = 0;
+    for (uint32_t k = 1; k <= b->K; ++k)
+        for (uint64_t q = 0; q < b->c[k]; ++q) dst[pos++] = (uint16_t)k;
+    memcpy(dst + pos, b->big, b->nb * sizeof(uint16_t));
+}
+
+/* Exponential::increase_nplus on the bin store: the same draws and checks as prolif_nplus. */
+static int prolif_nplus_bins(binstore* b, uint64_t* nminus, uint64_t cap, wstream* ws, int seg,
+                             uint32_t* idx_out, uint32_t* k1_out, int* uneven_out) {
+    const uint64_t L = b->ns + b->nb;
+    uint32_t i = ws_index(ws, (uint32_t)L);
+    uint32_t k = bins_get(b, i);
+    if (k > 32767u) return ECDNA_REP_ERR_OVERFLOW;
+    uint32_t n = 2u * k;
+    uint32_t k1;
+    int uneven;
+    int err = segregate(ws, seg, n, &k1, &uneven);
+    if (err) return err;
+    if (uneven == UNEVEN_FALSE && L + 1 > cap) return ECDNA_REP_ERR_CELL_CAP;
+    if (uneven == UNEVEN_FALSE) {
+        uint32_t d[2] = {k1, n - k1};
+        bins_replace(b, i, k, d, 2);
+    } else {
+        if (uneven == UNEVEN_TRUE) *nminus += 1;
+        uint32_t d[1] = {n};
+        bins_replace(b, i, k, d, 1);
+    }
+    *idx_out = i;
+    *k1_out = k1;
+    *uneven_out = uneven;
+    return 0;
+}
+
+/* CellDeath::decrease_nplus on the bin store. */
+static uint32_t death_nplus_bins(binstore* b, wstream* ws) {
+    uint32_t i = ws_index(ws, (uint32_t)(b->ns + b->nb));
+    bins_replace(b, i, bins_get(b, i), NULL, 0);
+    return i;
+}
+
 /* -------------------------------------------------------------- one run */
 
 typedef struct {
@@ -339,7 +448,18 @@ static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16
     const uint16_t* init;
     uint64_t nplus, nminus;
     init_of_set(p, set, &init, &nplus, &nminus);
-    memcpy(row, init, nplus * sizeof(uint16_t));
+    const int binned = (p->flags & ECDNA_FLAG_BIN_STORE) != 0;
+    binstore* bs = NULL;
+    uint16_t* snap_scratch = NULL;
+    if (binned) {
+        bs = calloc(1, sizeof(binstore));
+        bs->K = p->bin_kmax ? p->bin_kmax : 64;
+        bs->big = malloc(((size_t)p->cell_cap + 1) * sizeof(uint16_t));
+        for (uint64_t j = 0; j < nplus; ++j) bins_add(bs, init[j]);
+        if (snap_rows) snap_scratch = malloc(((size_t)p->cell_cap + 1) * sizeof(uint16_t));
+    } else {
+        memcpy(row, init, nplus * sizeof(uint16_t));
+    }
 
     memset(out, 0, sizeof(*out));
     uint64_t h = FNV_OFFSET;
@@ -381,9 +501,15 @@ static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16
             stop = ECDNA_STOP_ABSORBING;
             break;
         }
-        if (p->n_snapshots)
-            oracle_snapshot_check(p, &sj, nminus, nplus, f32t ? (double)t32 : t, row, snap_meta, snap_rows,
+        if (p->n_snapshots) {
+            const uint16_t* cur = row;
+            if (binned && snap_scratch) {
+                bins_expand(bs, snap_scratch);
+                cur = snap_scratch;
+            }
+            oracle_snapshot_check(p, &sj, nminus, nplus, f32t ? (double)t32 : t, cur, snap_meta, snap_rows,
                                   snap_stride);
+        }
         uint32_t w[4];
         event_block(p->seed, rid, e, w);
         /* direct method: channel by w1 against the cumulative propensities */
@@ -400,7 +526,13 @@ static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16
             case ECDNA_EV_PROLIF_NPLUS: {
                 uint32_t i, k1, k2;
                 int un;
-                int rc = prolif_nplus(row, &nplus, &nminus, p->cell_cap, &ws, p->segregation, &i, &k1, &k2, &un);
+                int rc;
+                if (binned) {
+                    rc = prolif_nplus_bins(bs, &nminus, p->cell_cap, &ws, p->segregation, &i, &k1, &un);
+                    nplus = bs->ns + bs->nb;
+                } else {
+                    rc = prolif_nplus(row, &nplus, &nminus, p->cell_cap, &ws, p->segregation, &i, &k1, &k2, &un);
+                }
                 if (rc) {
                     err = (uint32_t)rc;
                     stop = ECDNA_STOP_ERROR;
@@ -414,7 +546,13 @@ static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16
                 nminus -= 1;
                 break;
             default: { /* decrease_nplus (src/proliferation.rs:126-133) */
-                uint32_t i = death_nplus(row, &nplus, &ws);
+                uint32_t i;
+                if (binned) {
+                    i = death_nplus_bins(bs, &ws);
+                    nplus = bs->ns + bs->nb;
+                } else {
+                    i = death_nplus(row, &nplus, &ws);
+                }
                 x |= (uint64_t)i << 20;
                 break;
             }
@@ -426,6 +564,12 @@ static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16
         else
             t = t + tau; /* self.time += reaction.time (src/process.rs:184, 336) */
         if (hash_on) h = fnv_fold(h, x);
+    }
+    if (binned) {
+        bins_expand(bs, row);
+        free(bs->big);
+        free(bs);
+        free(snap_scratch);
     }
     out->nminus = nminus;
     out->nplus = nplus;
@@ -530,6 +674,8 @@ static int validate(const ecdna_ssa_params_t* p, uint64_t row_stride, int want_r
         if (!p->init_set_offsets) break;
     }
     if (maxn > p->cell_cap) return ECDNA_E_INVALID;
+    if ((p->flags & ECDNA_FLAG_BIN_STORE) && p->bin_kmax != 0 && p->bin_kmax != 64 && p->bin_kmax != 256)
+        return ECDNA_E_INVALID;
     if (want_rows && row_stride < p->cell_cap) return ECDNA_E_INVALID;
     if (p->n_snapshots > 64 || (p->n_snapshots && !p->snapshot_cells)) return ECDNA_E_INVALID;
     for (uint32_t q = 1; q < p->n_snapshots; ++q)

@@ -4,7 +4,13 @@ Each case is a small RunSpec the CPU oracle finishes in well under a second. Tog
 both processes, all four segregation rules, f32/f64 time, the birth-death cap-compat flag, single-
 and multi-set (ABC) runs, non-default initial distributions, replicate-id offsets (sharding) and
 every stop reason and per-replicate error the engine reports.
+
+bin_cases() runs the same cases through the bin store (ECDNA_FLAG_BIN_STORE), plus
+cases aimed at its boundaries: copy numbers around bin_kmax (daughters crossing it, picks from the
+large-k row, swap_remove inside it), the 256-bin variant and u32 counters (cell_cap > 65535).
 """
+import dataclasses
+
 from ecdna_evo_amd import abi
 
 H = abi.FLAG_EVENT_HASH
@@ -77,4 +83,30 @@ def cases():
                                     flags=S | abi.FLAG_TIME_F32)
     c["bd_snapshots_meta_only"] = abi.RunSpec(seed=30, process=abi.BIRTH_DEATH, rates=BD_RATES, n_replicates=32,
                                               max_cells=600, snapshots=abi.default_snapshots(600), flags=H)
+    return c
+
+
+def bin_cases():
+    B = abi.FLAG_BIN_STORE
+    c = {}
+    for name, spec in cases().items():
+        c[f"bins_{name}"] = dataclasses.replace(spec, flags=spec.flags | B, _keep=[])
+    for name in ("bd_turnover", "big_copies", "abc_sets", "bd_snapshots", "pb_binomial_c1"):
+        spec = cases()[name]
+        c[f"bins256_{name}"] = dataclasses.replace(spec, flags=spec.flags | B, bin_kmax=256, _keep=[])
+    c["bins_boundary_pb"] = abi.RunSpec(seed=41, n_replicates=32, max_cells=400, init={30: 2, 33: 1, 64: 2, 65: 2, 130: 1},
+                                        hist_bins=300, flags=H | B)
+    c["bins_boundary_bd"] = abi.RunSpec(seed=43, process=abi.BIRTH_DEATH, rates=((1.0, 1.3, 0.6, 0.7),),
+                                        n_replicates=32, max_cells=500, init={63: 3, 66: 4, 200: 2}, hist_bins=300,
+                                        flags=H | B)
+    c["bins_boundary_nonminus"] = abi.RunSpec(seed=44, segregation=abi.SEG_BINOMIAL_NO_NMINUS, n_replicates=32,
+                                              max_cells=300, init={1: 3, 40: 2, 70: 1}, hist_bins=300, flags=H | B)
+    c["bins256_boundary_bd"] = abi.RunSpec(seed=45, process=abi.BIRTH_DEATH, rates=((1.0, 1.3, 0.6, 0.7),),
+                                           n_replicates=32, max_cells=500, init={250: 3, 257: 4, 600: 1},
+                                           hist_bins=700, bin_kmax=256, flags=H | B)
+    c["bins_c32"] = abi.RunSpec(seed=46, process=abi.BIRTH_DEATH, rates=BD_RATES, n_replicates=32, max_cells=1500,
+                                cell_cap=70_000, init={1: 2, 70: 1}, flags=H | B)
+    c["bins256_c32"] = abi.RunSpec(seed=47, process=abi.BIRTH_DEATH, rates=((1.0, 1.0, 0.9, 0.9),), n_replicates=16,
+                                   max_cells=1300, max_time=3.0, cell_cap=70_000, init={1: 900, 80: 100},
+                                   bin_kmax=256, flags=H | B | abi.FLAG_SNAPSHOT_ROWS, snapshots=[950, 1000, 1100])
     return c

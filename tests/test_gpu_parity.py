@@ -7,9 +7,10 @@ swap_remove order, the pooled copy-number histograms and the per-set totals must
 import numpy as np
 import pytest
 
-from cases import cases
+from cases import bin_cases, cases
 
 CASES = cases()
+BIN_CASES = bin_cases()
 
 
 def _compare(gpu, cpu, name):
@@ -39,6 +40,17 @@ def _compare(gpu, cpu, name):
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_gpu_matches_oracle(name, engine_mod, oracle_mod):
     spec = CASES[name]
+    gpu = engine_mod.run(spec, want_rows=True)
+    cpu = oracle_mod.run(spec, mode="philox", want_rows=True)
+    _compare(gpu, cpu, name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(BIN_CASES))
+def test_gpu_bin_store_matches_oracle(name, engine_mod, oracle_mod):
+    """The bin store (ECDNA_FLAG_BIN_STORE) against the oracle's restatement of it, bit for bit; rows
+    in canonical order."""
+    spec = BIN_CASES[name]
     gpu = engine_mod.run(spec, want_rows=True)
     cpu = oracle_mod.run(spec, mode="philox", want_rows=True)
     _compare(gpu, cpu, name)
@@ -82,6 +94,25 @@ def test_gpu_grid_size_does_not_change_results(engine_mod, monkeypatch):
     b = engine_mod.run(spec)
     np.testing.assert_array_equal(a.summaries["event_hash"], b.summaries["event_hash"])
     np.testing.assert_array_equal(a.hist, b.hist)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kmax", [64, 256])
+def test_gpu_bin_store_grid_and_chunks_do_not_change_results(kmax, engine_mod, monkeypatch):
+    """Bin store: results depend on replicate ids only (lane refill, chunking)."""
+    from ecdna_evo_amd import abi
+
+    spec = abi.RunSpec(seed=31, process=abi.BIRTH_DEATH, rates=((1.0, 1.2, 0.8, 0.8),), n_replicates=3000,
+                       max_cells=300, init={1: 2, 70: 1}, bin_kmax=kmax,
+                       flags=abi.FLAG_EVENT_HASH | abi.FLAG_BIN_STORE)
+    a = engine_mod.run(spec)
+    monkeypatch.setenv("ECDNA_SSA_MAX_BLOCKS", "1")
+    b = engine_mod.run(spec)
+    monkeypatch.setenv("ECDNA_SSA_MAX_CHUNK", "101")
+    c = engine_mod.run(spec)
+    for r in (b, c):
+        np.testing.assert_array_equal(a.summaries["event_hash"], r.summaries["event_hash"])
+        np.testing.assert_array_equal(a.hist, r.hist)
 
 
 @pytest.mark.gpu

@@ -32,3 +32,12 @@ if __name__ == "__main__":
     if "c3" in which:
         probe("C3 BD 2^20x1e4", abi.RunSpec(seed=42, process=abi.BIRTH_DEATH, rates=((1.0, 1.5, 0.3, 0.3),),
                                             n_replicates=1 << 20, max_cells=10_000, flags=0))
+    if "c2bins" in which:
+        probe("C2 PB 65536x1e4 bins", abi.RunSpec(seed=42, n_replicates=65536, max_cells=10_000,
+                                                  flags=abi.FLAG_BIN_STORE))
+    if "c3bins1" in which:  # one launch only (profiling)
+        probe("C3 BD 2^20x1e4 bins", abi.RunSpec(seed=42, process=abi.BIRTH_DEATH, rates=((1.0, 1.5, 0.3, 0.3),),
+                                                 n_replicates=1 << 20, max_cells=10_000, flags=abi.FLAG_BIN_STORE), reps=1)
+    if "c3bins" in which:
+        probe("C3 BD 2^20x1e4 bins", abi.RunSpec(seed=42, process=abi.BIRTH_DEATH, rates=((1.0, 1.5, 0.3, 0.3),),
+                                                 n_replicates=1 << 20, max_cells=10_000, flags=abi.FLAG_BIN_STORE))

@@ -12,7 +12,8 @@ import os, sys, json, time
 sys.path.insert(0, os.path.join(%r, "ecdna-evo_amd"))
 from ecdna_evo_amd import abi, engine
 spec = abi.RunSpec(seed=42, process=abi.BIRTH_DEATH, rates=((1.0, 1.5, 0.3, 0.3),), reps_per_set=int(os.environ.get("SWEEP_REPS", 1 << 20)),
-                   n_replicates=int(os.environ.get("SWEEP_REPS", 1 << 20)), max_cells=10_000, flags=0)
+                   n_replicates=int(os.environ.get("SWEEP_REPS", 1 << 20)), max_cells=10_000,
+                   flags=int(os.environ.get("SWEEP_FLAGS", "0"), 0), bin_kmax=int(os.environ.get("SWEEP_KMAX", "0")))
 ctx = engine.Context(spec)
 ms = []
 for i in range(3):
