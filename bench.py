@@ -11,13 +11,19 @@ One step = one full run of the hot path on every GPU: zero outputs, the persiste
 kernel over all 2^20 replicates, the histogram kernel, and (N>1) the all-reduce. Inputs are
 resident in HBM before the timed region.
 
+Cell store (--store): "bins" (default, ECDNA_FLAG_BIN_STORE: per-replicate copy-number counters in
+LDS) or "rows" (one u16 per cell in HBM in the reference's swap_remove order). Both
+simulate the same process and count the same events; each is bit-exact with its oracle restatement.
+
 Extra JSON fields:
   roofline      — the stepper kernel against HBM: algorithmic bytes per launch over
                   its average duration (HIP events on the launch stream), vs 8 TB/s; `traffic` =
                   measured HBM bytes per launch from the committed rocprofv3 PMC summary, if present;
-                  `hbm_requests` = the same kernel against the random-access request ceiling that
-                  actually bounds it (requests per event from the PMC summary x events/s, vs the
-                  calibrated random read-modify-write rate).
+                  rows: `hbm_requests` = the same kernel against the random-access request ceiling that
+                  bounds it (requests per event from the PMC summary x events/s, vs the calibrated
+                  random read-modify-write rate); bins: `valu_issue` = its vector instructions per
+                  second against the chip's wave64 VALU issue rate, which bounds it (instructions per
+                  event from the PMC summary x events/s).
   cpu_baseline  — the reference-semantics CPU restatement (oracle/, ChaCha8 + first-reaction +
                   BTPE, "port") on a bounded sample of the same workload, rank 0 at N=1 only.
 """
@@ -41,12 +47,15 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 TB/s mea
 # algorithmic bytes per event: per-cell u16 row with swap_remove
 B_PROLIF_EVEN, B_PROLIF_UNEVEN, B_DEATH_NPLUS = 10, 8, 6
 B_SUMMARY = 88
+# wave64 VALU instructions the chip can issue per second: 256 CUs x 4 SIMD-32 x 2.4 GHz / 2 cycles
+# (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles")
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2
 
 
-def workload_spec(first: int, n: int, total: int, seed: int = 42, device: int = 0) -> abi.RunSpec:
+def workload_spec(first: int, n: int, total: int, seed: int = 42, device: int = 0, store: str = "bins") -> abi.RunSpec:
     return abi.RunSpec(process=abi.BIRTH_DEATH, segregation=abi.SEG_BINOMIAL, rates=((1.0, 1.5, 0.3, 0.3),),
                        reps_per_set=total, seed=seed, first_replicate=first, n_replicates=n, max_cells=10_000,
-                       hist_bins=1025, flags=0, device=device)
+                       hist_bins=1025, flags=abi.FLAG_BIN_STORE if store == "bins" else 0, device=device)
 
 
 def algorithmic_bytes(words, n_reps: int, init_cells: int = 1) -> int:
@@ -57,10 +66,10 @@ def algorithmic_bytes(words, n_reps: int, init_cells: int = 1) -> int:
             + n_reps * (2 * init_cells + B_SUMMARY))
 
 
-def load_pmc():
-    """The committed rocprofv3 PMC summary of the stepper on this workload (profiles/pmc_c3.json)."""
+def load_pmc(store: str):
+    """The committed rocprofv3 PMC summary of the stepper on this workload (profiles/pmc_c3[_bins].json)."""
     try:
-        with open(os.path.join(REPO, "profiles", "pmc_c3.json")) as f:
+        with open(os.path.join(REPO, "profiles", "pmc_c3_bins.json" if store == "bins" else "pmc_c3.json")) as f:
             return json.load(f)
     except Exception:
         return {}
@@ -124,6 +133,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--reps-per-gpu", type=int, default=REPS_PER_GPU)
+    ap.add_argument("--store", choices=("bins", "rows"), default="bins")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -141,7 +151,7 @@ def main():
     total = reps * n_gpus
 
     first, n = shard.weak_range(rank, reps)
-    spec = workload_spec(first, n, total, device=local if distributed else 0)
+    spec = workload_spec(first, n, total, device=local if distributed else 0, store=args.store)
     ctx = engine.Context(spec)
     hist = torch.zeros(spec.hist_bins, dtype=torch.int64, device="cuda")
     tot = torch.zeros(16, dtype=torch.int64, device="cuda")
@@ -196,11 +206,23 @@ def main():
     if rank == 0:
         avg_kernel_s = sum(kernel_ms) / len(kernel_ms) * 1e-3
         achieved = local_alg / avg_kernel_s / 1e9
-        pmc = load_pmc()
+        pmc = load_pmc(args.store)
         traffic = pmc.get("hbm_bytes_per_launch")
         kernel_eps = local_events / avg_kernel_s
         transactions = None
-        if "read_requests_per_event" in pmc:
+        issue = None
+        if args.store == "bins" and "valu_insts_per_event" in pmc:
+            per_event = pmc["valu_insts_per_event"]
+            issue = {
+                "valu_wave_insts_per_event": per_event,
+                "per_s": per_event * kernel_eps,
+                "peak_per_s": VALU_ISSUE_PEAK,
+                "frac": per_event * kernel_eps / VALU_ISSUE_PEAK,
+                "note": "the bin store keeps every common-case event in LDS and registers, so the stepper is "
+                        "bounded by vector-instruction issue, not HBM (DESIGN.md §5); wave64 VALU instructions "
+                        "per event (= per lane-event / 64) from the committed PMC summary (SQ_INSTS_VALU)",
+            }
+        if args.store == "rows" and "read_requests_per_event" in pmc:
             per_event = pmc["read_requests_per_event"] + pmc["write_requests_per_event"]
             ceiling = rmw_ceiling()
             transactions = {
@@ -229,10 +251,13 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u16+f64",
+            "store": args.store,
             "data": "synthetic",
             "config": {
                 "workload": "C3 (BASELINE.json configs[2]): 2^20 replicates/GPU, birth-death b0=1 b1=1.5 "
                             "d0=d1=0.3, binomial segregation, init {1:1}, stop 1e4 cells or t=17, seed 42",
+                "cell_store": "bins (copy-number counters in LDS, k<=64; ECDNA_FLAG_BIN_STORE)" if args.store == "bins"
+                              else "rows (u16 per cell in HBM, swap_remove order)",
                 "replicates_per_gpu": reps,
                 "replicates_total": total,
                 "events_per_step": events_per_step,
@@ -250,6 +275,7 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "hbm_requests": transactions,
+                "valu_issue": issue,
             },
             "cpu_baseline": cpu,
         }

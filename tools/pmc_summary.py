@@ -2,7 +2,8 @@
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats (same command as bench.py)
   profiles/<tag>_bench.json         the bench line of that session
   profiles/<tag>_pmc.json           stepper FETCH_SIZE / WRITE_SIZE per launch and per event
-  profiles/pmc_c3.json              the latest of the above, read by bench.py for roofline.traffic
+  profiles/pmc_c3.json / pmc_c3_bins.json  the latest of the above for the row / bin store, read by
+                                    bench.py for roofline.traffic and the hbm_requests / valu_issue views
   profiles/<tag>_pmc_calibration.json  bytes per access of the calibration kernels
 Usage: python tools/pmc_summary.py gpurun_out/prof_<tag> <tag>
 """
@@ -27,19 +28,27 @@ def main(src, tag):
     shutil.copy(os.path.join(src, "bench.json"), os.path.join(prof, f"{tag}_bench.json"))
     kstats = {r["Name"]: float(r["AverageNs"]) for r in rows(os.path.join(src, "kt", "kt_kernel_stats.csv"))}
     pmc = {}
-    for counter, sub in (("FETCH_SIZE", "pmc_fetch"), ("WRITE_SIZE", "pmc_write")):
-        for r in rows(os.path.join(src, sub, "pmc_counter_collection.csv")):
-            if r["Kernel_Name"] in ("ssa_stepper", "ssa_hist"):
+    kname = "ssa_stepper_bins" if bench.get("store") == "bins" else "ssa_stepper"
+    for counter, sub in (("FETCH_SIZE", "pmc_fetch"), ("WRITE_SIZE", "pmc_write"), (None, "pmc_sq")):
+        path = os.path.join(src, sub, "pmc_counter_collection.csv")
+        if not os.path.exists(path):
+            continue
+        for r in rows(path):
+            if r["Kernel_Name"] in (kname, "ssa_hist"):
                 d = pmc.setdefault(r["Kernel_Name"], {})
-                d[counter + "_bytes"] = float(r["Counter_Value"]) * 1024.0
+                if counter:
+                    d[counter + "_bytes"] = float(r["Counter_Value"]) * 1024.0
+                else:
+                    d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
                 d.update(VGPR_Count=int(r["VGPR_Count"]), SGPR_Count=int(r["SGPR_Count"]),
                          LDS_Block_Size=int(r["LDS_Block_Size"]), Grid_Size=int(r["Grid_Size"]))
     ev = bench["config"]["events_per_step"]
-    st = pmc["ssa_stepper"]
+    st = pmc[kname]
     out = {
         "round": tag,
         "workload": bench["config"]["workload"],
-        "kernel": "ssa_stepper",
+        "store": bench.get("store", "rows"),
+        "kernel": kname,
         "events_per_launch": ev,
         "FETCH_SIZE_bytes_per_launch": st["FETCH_SIZE_bytes"],
         "WRITE_SIZE_bytes_per_launch": st["WRITE_SIZE_bytes"],
@@ -48,21 +57,29 @@ def main(src, tag):
         "write_bytes_per_event": st["WRITE_SIZE_bytes"] / ev,
         "read_requests_per_event": st["FETCH_SIZE_bytes"] / ev / 64.0,
         "write_requests_per_event": st["WRITE_SIZE_bytes"] / ev / 32.0,
-        "stepper_avg_ns_rocprof": kstats.get("ssa_stepper"),
+        "stepper_avg_ns_rocprof": kstats.get(kname),
         "stepper_avg_ms_hip_events": bench["config"]["kernel_ms_avg"],
         "transactions_per_s": (st["FETCH_SIZE_bytes"] / 64.0 + st["WRITE_SIZE_bytes"] / 32.0)
-        / (kstats["ssa_stepper"] * 1e-9),
+        / (kstats[kname] * 1e-9),
         "correction": "none: the stepper makes no wide streaming reads (the gfx950 x2 FETCH_SIZE correction "
                       "applies to 16-B/lane coalesced reads, reproduced by the calibration stream_load_x4 "
                       "ratio 0.5); on this access shape one random 2-B load = one 64-B read request and one "
                       "random 2-B store = one 32-B write request (calibration file)",
         "launch": {k: st[k] for k in ("VGPR_Count", "SGPR_Count", "LDS_Block_Size", "Grid_Size")},
+        "sq": {k: st[k] for k in st if k.startswith("SQ_")},
         "ssa_hist": pmc.get("ssa_hist"),
         "source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of "
                   "`python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline` (tools/gpu_profile.sh)",
     }
+    if "SQ_INSTS_VALU" in st:
+        # SQ_INSTS_VALU counts wave instructions; one wave-event = 64 lane-events
+        out["valu_insts_per_event"] = st["SQ_INSTS_VALU"] / ev
+        out["valu_wave_insts_per_wave_event"] = st["SQ_INSTS_VALU"] / (ev / 64.0)
+        out["salu_wave_insts_per_wave_event"] = st.get("SQ_INSTS_SALU", 0.0) / (ev / 64.0)
+        out["lds_wave_insts_per_wave_event"] = st.get("SQ_INSTS_LDS", 0.0) / (ev / 64.0)
     json.dump(out, open(os.path.join(prof, f"{tag}_pmc.json"), "w"), indent=1)
-    json.dump(out, open(os.path.join(prof, "pmc_c3.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(prof, "pmc_c3_bins.json" if out["store"] == "bins" else "pmc_c3.json"), "w"),
+              indent=1)
     cal = {}
     for counter, sub in (("FETCH_SIZE", "calib_fetch"), ("WRITE_SIZE", "calib_write")):
         p = os.path.join(src, sub, "pmc_counter_collection.csv")
