@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "ssa_logtab.h"
+
 #pragma clang fp contract(off)
 
 namespace ecdna {
@@ -21,7 +23,7 @@ constexpr uint32_t kPhiloxW0 = 0x9E3779B9u;
 constexpr uint32_t kPhiloxW1 = 0xBB67AE85u;
 
 // Philox4x32-10. The key is wave-uniform (the run's seed), so the key schedule lives in SGPRs;
-// each round is two 32x32->64 multiplies and four XORs per lane.
+// each round is two 32x32->64 multiplies (v_mad_u64_u32) and four XORs per lane (gfx9 has no v_xor3).
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
@@ -40,31 +42,35 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1
     return c;
 }
 
-// -ln((w + 0.5) 2^-32): same operations, same order as oracle_softlog_neg (oracle/ssa_oracle.c).
-__device__ __forceinline__ double softlog_neg(uint32_t w) {
-    const uint64_t m = 2ull * (uint64_t)w + 1ull;
-    int ex = 63 - __clzll((long long)m);
-    const double d = (double)m;
-    const double scale = __longlong_as_double((long long)((uint64_t)(1023 - ex) << 52));
-    double f = d * scale;
-    if (f > 0x1.6a09e667f3bcdp+0) {
-        f = f * 0.5;
-        ex += 1;
-    }
-    const double s = (f - 1.0) / (f + 1.0);
-    const double z = s * s;
-    double r = 0x1.af286bca1af28p-5;
-    r = r * z + 0x1.e1e1e1e1e1e1ep-5;
-    r = r * z + 0x1.1111111111111p-4;
-    r = r * z + 0x1.3b13b13b13b14p-4;
-    r = r * z + 0x1.745d1745d1746p-4;
-    r = r * z + 0x1.c71c71c71c71cp-4;
-    r = r * z + 0x1.2492492492492p-3;
-    r = r * z + 0x1.999999999999ap-3;
-    r = r * z + 0x1.5555555555555p-2;
-    const double s2 = s + s;
-    const double lnf = s2 + (s2 * z) * r;
-    return (double)(33 - ex) * 0x1.62e42fefa39efp-1 - lnf;
+// -ln((w + 0.5) 2^-32), draw mapping v2: d = w + 0.5 = m 2^ex with m in [0.5, 1); the
+// top 7 fraction bits j of m pick {C, LN} = {1/mid_j, ln mid_j} (ssa_logtab.h, staged in LDS), r =
+// m C - 1 (|r| <= 2^-8, the subtraction exact), ln(1 + r) by a degree-7 series in explicit fmas, and
+// -ln u = -(LN + ln(1 + r) + (ex - 32) ln 2). oracle_softlog_neg (oracle/ssa_oracle.c) performs the
+// same IEEE operations in the same order, so CPU and GPU agree bit for bit.
+__device__ __forceinline__ double softlog_neg(uint32_t w, const double2* tab) {
+    const double d = (double)w + 0.5;  // exact
+    const uint64_t bits = (uint64_t)__double_as_longlong(d);
+    const uint32_t hi = (uint32_t)(bits >> 32);
+    const int ex = (int)(hi >> 20) - 1022;
+    const double m = __longlong_as_double((long long)((bits & 0x000fffffffffffffull) | (1022ull << 52)));
+    const double2 cl = tab[(hi >> 13) & 127u];
+    const double r = m * cl.x - 1.0;
+    double q = fma(r, 0x1.2492492492492p-3, -0x1.5555555555555p-3);  // 1/7, -1/6
+    q = fma(r, q, 0x1.999999999999ap-3);                                // 1/5
+    q = fma(r, q, -0x1p-2);                                             // -1/4
+    q = fma(r, q, 0x1.5555555555555p-2);                                // 1/3
+    q = fma(r, q, -0x1p-1);                                             // -1/2
+    const double l = fma(r * r, q, r);                                  // ln(1 + r)
+    return -fma((double)(ex - 32), 0x1.62e42fefa39efp-1, cl.y + l);
+}
+
+// The log table in constant memory; each workgroup stages it into LDS (divergent per-lane index).
+__constant__ const double kLogTab[2 * ECDNA_LOGTAB_N] = ECDNA_LOGTAB_INIT;
+
+__device__ __forceinline__ void stage_logtab(double2* lds) {
+    for (uint32_t i = threadIdx.x; i < ECDNA_LOGTAB_N; i += blockDim.x)
+        lds[i] = make_double2(kLogTab[2 * i], kLogTab[2 * i + 1]);
+    __syncthreads();
 }
 
 // Extra words of one event: [w2, w3, blk1.x..w, blk2.x..w, ...], blk j = Philox(e, j, rid).

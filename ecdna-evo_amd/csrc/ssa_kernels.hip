@@ -48,6 +48,8 @@ constexpr uint32_t kFlush = 16;
 template <bool BD, int SEG, bool WIN>
 __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a) {
     __shared__ uint16_t win[WIN ? kWin + 1 : 1][kStepperBlock];  // + 1 spare row
+    __shared__ double2 logtab[ECDNA_LOGTAB_N];
+    stage_logtab(logtab);
     const uint32_t tid = threadIdx.x;
     const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
     const bool f32t = (a.flags & ECDNA_FLAG_TIME_F32) != 0;
@@ -322,7 +324,7 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
         }
 
         // waiting time
-        const double tau = softlog_neg(w.x) / a0;
+        const double tau = softlog_neg(w.x, logtab) / a0;
 
         uint64_t x = ch;
         if (ch == 1u) {
@@ -403,32 +405,35 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
     constexpr uint32_t K = L::kK;
     __shared__ uint4 cnt_v[L::kBinVecs][BLK];  // bin counters
     __shared__ uint4 sum_v[L::kSumVecs][BLK];  // group sums
+    __shared__ double2 logtab[ECDNA_LOGTAB_N];
+    stage_logtab(logtab);
     const uint32_t tid = threadIdx.x;
     const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
     const bool f32t = (a.flags & ECDNA_FLAG_TIME_F32) != 0;
     const bool hash_on = (a.flags & ECDNA_FLAG_EVENT_HASH) != 0;
 
-    // packed counter add: bin b (0-based, copy number b + 1) / group g, by +1 or -1 (two's complement
-    // on the 32-bit word: a 16-bit field never borrows from its neighbour because it is >= 1 when
-    // decremented)
-    auto word_of_bin = [&](uint32_t b) -> uint32_t* {
+    // packed counter add: bin b (0-based, copy number b + 1) / group g, by +d (d = +1, -1 or 0, as a
+    // two's complement 32-bit word: a 16-bit field never borrows from its neighbour because it is >= 1
+    // when decremented)
+    auto bin_word = [&](uint32_t b) -> uint32_t* {
         const uint32_t v = C32 ? (b >> 2) : (b >> 3);
         const uint32_t w = C32 ? (b & 3u) : ((b & 7u) >> 1);
         return reinterpret_cast<uint32_t*>(&cnt_v[v][tid]) + w;
     };
-    auto word_of_group = [&](uint32_t g) -> uint32_t* {
+    auto group_word = [&](uint32_t g) -> uint32_t* {
         const uint32_t v = C32 ? (g >> 2) : (g >> 3);
         const uint32_t w = C32 ? (g & 3u) : ((g & 7u) >> 1);
         return reinterpret_cast<uint32_t*>(&sum_v[v][tid]) + w;
     };
-    auto unit = [&](uint32_t idx) -> uint32_t { return C32 ? 1u : (1u << ((idx & 1u) * 16)); };
-    auto bin_add = [&](uint32_t k, bool inc) {  // k in 1..K
+    auto shifted = [&](uint32_t idx, uint32_t d) -> uint32_t { return C32 ? d : (d << ((idx & 1u) * 16)); };
+    // bin of copy number k (1..K) += d (d in {1, 0xffffffff, 0}); unconditional LDS atomics, so lanes
+    // with nothing to change add 0 instead of branching
+    auto bin_add = [&](uint32_t k, uint32_t d) {
         const uint32_t b = k - 1, g = b >> 3;
-        const uint32_t ub = unit(b), ug = unit(g);
-        atomicAdd(word_of_bin(b), inc ? ub : 0u - ub);
-        atomicAdd(word_of_group(g), inc ? ug : 0u - ug);
+        atomicAdd(bin_word(b), shifted(b, d));
+        atomicAdd(group_word(g), shifted(g, d));
     };
-    // canonical position i < ns -> copy number
+    // canonical position i -> copy number, valid for i < ns (other lanes get an unused in-range value)
     auto bin_find = [&](uint32_t i) -> uint32_t {
         uint32_t run = 0, g = 0, base = 0;
 #pragma unroll
@@ -443,6 +448,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                 base = le ? run : base;
             }
         }
+        g = g < (uint32_t)NG ? g : (uint32_t)NG - 1u;
         const uint32_t r = i - base;
         uint32_t run2 = 0, b = 0;
 #pragma unroll
@@ -454,6 +460,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                 b += (run2 <= r) ? 1u : 0u;
             }
         }
+        b = b < 8u ? b : 7u;
         return g * 8u + b + 1u;
     };
     auto bins_zero = [&]() {
@@ -467,7 +474,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
         uint32_t pos = 0;
 #pragma unroll 1
         for (uint32_t b = 0; b < K; ++b) {
-            const uint32_t c = C32 ? *word_of_bin(b) : ((*word_of_bin(b) >> ((b & 1u) * 16)) & 0xffffu);
+            const uint32_t c = C32 ? *bin_word(b) : ((*bin_word(b) >> ((b & 1u) * 16)) & 0xffffu);
 #pragma unroll 1
             for (uint32_t q = 0; q < c; ++q) dst[pos++] = (uint16_t)(b + 1u);
         }
@@ -480,7 +487,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
     uint64_t rid = 0;
     uint16_t* row = a.rows;
     uint32_t nm = 0, ns = 0, nb = 0;
-    float b0 = 0.f, b1 = 0.f, d0 = 0.f, d1 = 0.f;
+    double rb0 = 0.0, rb1 = 0.0, rd0 = 0.0, rd1 = 0.0;  // the f32 rates, widened once per replicate
     double t = 0.0;
     float t32 = 0.f;
     uint32_t e = 0, n_pm = 0, n_pp = 0, n_dm = 0, n_dp = 0, n_un = 0;
@@ -489,7 +496,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
     uint32_t sj = 0;
 
     for (;;) {
-        if (!active) {
+        if (!active) {  // ---- replicate boundary (rare): write the finished one, pull the next
             if (have) {
                 // final bin counters -> bags[li] (B stays in the row)
                 uint4* bag = reinterpret_cast<uint4*>(a.bags) + (uint64_t)li * L::kBinVecs;
@@ -518,10 +525,10 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             row = a.rows + (uint64_t)i * a.row_stride;
             const uint64_t set = rid / a.reps_per_set;
             const float4 r = a.rates[set];
-            b0 = r.x;
-            b1 = r.y;
-            d0 = r.z;
-            d1 = r.w;
+            rb0 = (double)r.x;
+            rb1 = (double)r.y;
+            rd0 = (double)r.z;
+            rd1 = (double)r.w;
             const uint16_t* src = a.init_copies;
             uint32_t cnt = a.init_nplus;
             if (a.init_offsets) {
@@ -534,7 +541,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             for (uint32_t j = 0; j < cnt; ++j) {
                 const uint32_t kk = src[j];
                 if (kk <= K) {
-                    bin_add(kk, true);
+                    bin_add(kk, 1u);
                     ++ns;
                 } else {
                     row[nb++] = (uint16_t)kk;
@@ -558,16 +565,13 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
         const uint32_t np = ns + nb;
 
         // propensities rate_i * population_i over [n-, n+(, n-, n+)]
-        const double pa = (double)b0 * (double)nm;
-        const double pb = (double)b1 * (double)np;
-        const double cA = pa;
-        const double cB = cA + pb;
+        const double fm = (double)nm, fp = (double)np;
+        const double cA = rb0 * fm;
+        const double cB = cA + rb1 * fp;
         double cC = cB, a0 = cB;
         if (BD) {
-            const double pc = (double)d0 * (double)nm;
-            const double pd = (double)d1 * (double)np;
-            cC = cB + pc;
-            a0 = cC + pd;
+            cC = cB + rd0 * fm;
+            a0 = cC + rd1 * fp;
         }
         {
             const bool t_over = f32t ? (t32 >= a.max_time32) : (t >= a.max_time);
@@ -600,12 +604,13 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
 
         const uint32_t rid_lo = (uint32_t)rid, rid_hi = (uint32_t)(rid >> 32);
         const uint4 w = philox4x32_10(make_uint4(e, 0u, rid_lo, rid_hi), k0, k1);
+        // direct method: the channel is the number of cumulative propensities <= target (the first i
+        // with target < c_i; the c_i are non-decreasing)
         const double target = (((double)w.y + 0.5) * 0x1p-32) * a0;
-        uint32_t ch;
-        if (BD)
-            ch = target < cA ? 0u : (target < cB ? 1u : (target < cC ? 2u : 3u));
-        else
-            ch = target < cA ? 0u : 1u;
+        uint32_t ch = (target >= cA ? 1u : 0u);
+        if (BD) ch += (target >= cB ? 1u : 0u) + (target >= cC ? 1u : 0u);
+        const bool nplus_ev = (ch & 1u) != 0;  // ProliferateNPlus or DeathNPlus: a cell is picked
+        const bool prolif = ch == 1u;
 
         WordStream ws;
         ws.w2 = w.z;
@@ -619,104 +624,88 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
         ws.blk_id = 0;
         ws.blk = make_uint4(0, 0, 0, 0);
 
-        uint32_t idx = 0, k = 0;
-        bool small = true;
-        if (ch & 1u) {
-            uint64_t m = (uint64_t)w.z * np;
-            uint32_t lo = (uint32_t)m;
-            if (lo < np) {
-                const uint32_t thr = (0u - np) % np;
-                while (lo < thr) {
-                    m = (uint64_t)ws.next() * np;
-                    lo = (uint32_t)m;
-                }
-            }
-            idx = (uint32_t)(m >> 32);
-            small = idx < ns;
-            if (small)
-                k = bin_find(idx);
-            else
-                k = gload_u16(row + (idx - ns));
+        // uniform N+ cell: Lemire multiply-shift on w2; exact rejection (rare) from the stream
+        uint64_t m = (uint64_t)w.z * np;
+        if (nplus_ev && (uint32_t)m < np) {
+            const uint32_t thr = (0u - np) % np;
+            while ((uint32_t)m < thr) m = (uint64_t)ws.next() * np;
         }
+        const uint32_t idx = (uint32_t)(m >> 32);
+        const bool small = idx < ns;
+        uint32_t k = bin_find(small ? idx : 0u);
+        if (nplus_ev && !small) k = gload_u16(row + (idx - ns));  // large-k row (rare)
 
-        uint32_t n = 0, k1v = 0;
-        uint32_t un = 0;
-        if (ch == 1u) {
-            if (k > 32767u) {  // checked_mul panic (src/proliferation.rs:63-67)
-                err = ECDNA_REP_ERR_OVERFLOW;
-                stop = ECDNA_STOP_ERROR;
-                active = false;
-                continue;
-            }
-            n = 2u * k;
-            if (SEG == ECDNA_SEG_DETERMINISTIC) {
-                k1v = k;
-            } else {
-                if (ws.pos == 1 && n <= 32u) {
-                    k1v = __popc(n == 32u ? w.w : (w.w & ((1u << n) - 1u)));
-                    ws.pos = 2;
-                } else {
-                    k1v = ws.binomial_half(n);
-                }
+        // Exponential::increase_nplus (src/proliferation.rs:25-111): its draws and error checks
+        const uint32_t n = 2u * k;
+        uint32_t k1v = k;
+        uint32_t un = 0;  // 0 False, 1 True, 2 TrueWithoutNMinusIncrease
+        uint32_t ev_err = 0;
+        if (SEG != ECDNA_SEG_DETERMINISTIC) {
+            const bool fast = ws.pos == 1 && n <= 32u;
+            k1v = __popc(w.w & (n >= 32u ? 0xffffffffu : ((1u << (n & 31u)) - 1u)));
+            if (prolif && !fast && k <= 32767u) {  // copy numbers > 16 or a rejected pick: more stream words
+                k1v = ws.binomial_half(n);
                 if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN) {
                     uint32_t tries = 1;
-                    bool rej = false;
                     while (k1v == 0u || k1v == n) {
                         if (tries == kNoUnevenMaxTries) {
-                            rej = true;
+                            ev_err = ECDNA_REP_ERR_REJECTION;
                             break;
                         }
                         k1v = ws.binomial_half(n);
                         ++tries;
                     }
-                    if (rej) {
-                        err = ECDNA_REP_ERR_REJECTION;
-                        stop = ECDNA_STOP_ERROR;
-                        active = false;
-                        continue;
+                }
+            } else if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN && prolif) {
+                uint32_t tries = 1;
+                ws.pos = 2;
+                while (k1v == 0u || k1v == n) {
+                    if (tries == kNoUnevenMaxTries) {
+                        ev_err = ECDNA_REP_ERR_REJECTION;
+                        break;
                     }
-                } else if (k1v == 0u || k1v == n) {
-                    un = (SEG == ECDNA_SEG_BINOMIAL_NO_NMINUS) ? 2u : 1u;
+                    k1v = ws.binomial_half(n);
+                    ++tries;
                 }
             }
-            if (un == 0u && np + 1u > a.cell_cap) {
-                err = ECDNA_REP_ERR_CELL_CAP;
-                stop = ECDNA_STOP_ERROR;
-                active = false;
-                continue;
-            }
+            if (SEG != ECDNA_SEG_BINOMIAL_NO_UNEVEN)
+                un = (k1v == 0u || k1v == n) ? (SEG == ECDNA_SEG_BINOMIAL_NO_NMINUS ? 2u : 1u) : 0u;
+        }
+        // checked_mul panic (src/proliferation.rs:63-67), then the row-capacity check
+        ev_err = (k > 32767u) ? (uint32_t)ECDNA_REP_ERR_OVERFLOW : ev_err;
+        ev_err = (ev_err == 0u && un == 0u && np + 1u > a.cell_cap) ? (uint32_t)ECDNA_REP_ERR_CELL_CAP : ev_err;
+        if (prolif && ev_err) {
+            err = ev_err;
+            stop = ECDNA_STOP_ERROR;
+            active = false;
+            continue;
         }
 
-        const double tau = softlog_neg(w.x) / a0;
+        const double tau = softlog_neg(w.x, logtab) / a0;
 
-        uint64_t x = ch;
-        if (ch & 1u) {
-            // daughters (none for a death): [k1, k2] on an even split, [n] on an uneven one
-            const bool prolif = ch == 1u;
-            const uint32_t da = (un == 0u) ? k1v : n;
-            const uint32_t db = n - k1v;
-            const bool has_a = prolif, has_b = prolif && un == 0u;
-            if (small) {
-                bin_add(k, false);
-                ns -= 1;
-            }
-            uint32_t open = small ? 0xffffffffu : idx - ns;  // B slot freed by a large picked cell
-            if (has_a) {
-                if (da <= K) {
-                    bin_add(da, true);
-                    ns += 1;
-                } else if (open != 0xffffffffu) {
+        // daughters (none for a death): [k1, k2] on an even split, [n] on an uneven one
+        const uint32_t da = (un == 0u) ? k1v : n;
+        const uint32_t db = n - k1v;
+        const bool has_a = prolif, has_b = prolif && un == 0u;
+        const bool sa = has_a && da <= K, sb = has_b && db <= K;
+        const uint32_t ns_old = ns;
+        // common case: every copy number involved is binned -> LDS only, no branch
+        bin_add(small ? k : 1u, (nplus_ev && small) ? 0xffffffffu : 0u);
+        bin_add(sa ? da : 1u, sa ? 1u : 0u);
+        bin_add(sb ? db : 1u, sb ? 1u : 0u);
+        ns = ns - ((nplus_ev && small) ? 1u : 0u) + (sa ? 1u : 0u) + (sb ? 1u : 0u);
+        if (nplus_ev && (!small || (has_a && !sa) || (has_b && !sb))) {  // the large-k row (rare)
+            uint32_t open = small ? 0xffffffffu : idx - ns_old;  // B slot freed by a large picked cell
+            if (has_a && !sa) {
+                if (open != 0xffffffffu) {
                     row[open] = (uint16_t)da;
                     open = 0xffffffffu;
                 } else {
                     row[nb++] = (uint16_t)da;
                 }
             }
-            if (has_b) {
-                if (db <= K) {
-                    bin_add(db, true);
-                    ns += 1;
-                } else if (open != 0xffffffffu) {
+            if (has_b && !sb) {
+                if (open != 0xffffffffu) {
                     row[open] = (uint16_t)db;
                     open = 0xffffffffu;
                 } else {
@@ -727,17 +716,9 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                 if (open != nb - 1) row[open] = (uint16_t)gload_u16(row + nb - 1);
                 nb -= 1;
             }
-            if (prolif) {
-                if (un != 0u) {
-                    nm += (un == 1u) ? 1u : 0u;
-                    n_un += 1;
-                }
-                x |= ((uint64_t)k1v << 2) | ((uint64_t)idx << 20);
-            } else {
-                x |= (uint64_t)idx << 20;
-            }
         }
-        nm = nm + (ch == 0u ? 1u : 0u) - ((BD && ch == 2u) ? 1u : 0u);
+        nm = nm + ((ch == 0u || (prolif && un == 1u)) ? 1u : 0u) - ((BD && ch == 2u) ? 1u : 0u);
+        n_un += (prolif && un != 0u) ? 1u : 0u;
         n_pm += ch == 0u ? 1u : 0u;
         n_pp += ch == 1u ? 1u : 0u;
         n_dm += ch == 2u ? 1u : 0u;
@@ -747,7 +728,11 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             t32 = t32 + (float)tau;
         else
             t = t + tau;
-        if (hash_on) h = (h ^ x) * kFnvPrime;
+        if (hash_on) {
+            const uint64_t x = (uint64_t)ch | (prolif ? ((uint64_t)k1v << 2) : 0ull) |
+                               (nplus_ev ? ((uint64_t)idx << 20) : 0ull);
+            h = (h ^ x) * kFnvPrime;
+        }
     }
 }
 

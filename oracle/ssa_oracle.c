@@ -29,7 +29,9 @@
  * times and channel picks bit for bit.
  */
 #include "ssa_oracle.h"
+#include "ssa_logtab.h"
 
+#include <math.h>
 #include <pthread.h>
 #include <stdatomic.h>
 #include <stdlib.h>
@@ -71,37 +73,32 @@ void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t
 
 /* -------------------------------------------------------------- soft log */
 
-/* -ln(u), u = (w + 0.5) * 2^-32 = (2w + 1) * 2^-33.
- * ln(m) for m = 2w+1 in [1, 2^33): m = 2^ex * f, f folded into (sqrt(2)/2, sqrt(2)],
- * ln f = 2 atanh(s), s = (f-1)/(f+1), series to s^19. Fixed operation order. */
+/* -ln(u), u = (w + 0.5) * 2^-32: the engine's draw mapping v2. d = w + 0.5 (exact) =
+ * m 2^ex with m in [0.5, 1); the top 7 fraction bits j of m select {C, LN} = {RN(1/mid_j), RN(ln mid_j)}
+ * (ssa_logtab.h, tools/gen_logtab.py); r = m C - 1 (|r| <= 2^-8); ln(1 + r) by a degree-7 series in
+ * explicit fma (C99 fma is the correctly rounded fused operation, like v_fma_f64); -ln u =
+ * -(LN + ln(1 + r) + (ex - 32) ln 2). Fixed operation order. */
+static const double LOGTAB[2 * ECDNA_LOGTAB_N] = ECDNA_LOGTAB_INIT;
+
 double oracle_softlog_neg(uint32_t w) {
-    uint64_t m = 2u * (uint64_t)w + 1u;
-    int ex = 63 - __builtin_clzll(m);
-    double d = (double)m; /* exact: m < 2^33 */
-    union {
-        double f;
-        uint64_t u;
-    } sc;
-    sc.u = (uint64_t)(1023 - ex) << 52; /* 2^-ex, exact */
-    double f = d * sc.f;                /* exact, in [1, 2) */
-    if (f > 0x1.6a09e667f3bcdp+0) {
-        f = f * 0.5;
-        ex += 1;
-    }
-    double s = (f - 1.0) / (f + 1.0);
-    double z = s * s;
-    double r = 0x1.af286bca1af28p-5;     /* 1/19 */
-    r = r * z + 0x1.e1e1e1e1e1e1ep-5;    /* 1/17 */
-    r = r * z + 0x1.1111111111111p-4;    /* 1/15 */
-    r = r * z + 0x1.3b13b13b13b14p-4;    /* 1/13 */
-    r = r * z + 0x1.745d1745d1746p-4;    /* 1/11 */
-    r = r * z + 0x1.c71c71c71c71cp-4;    /* 1/9 */
-    r = r * z + 0x1.2492492492492p-3;    /* 1/7 */
-    r = r * z + 0x1.999999999999ap-3;    /* 1/5 */
-    r = r * z + 0x1.5555555555555p-2;    /* 1/3 */
-    double s2 = s + s;
-    double lnf = s2 + (s2 * z) * r;
-    return (double)(33 - ex) * 0x1.62e42fefa39efp-1 - lnf;
+    const double d = (double)w + 0.5;
+    uint64_t bits;
+    memcpy(&bits, &d, sizeof bits);
+    const uint32_t hi = (uint32_t)(bits >> 32);
+    const int ex = (int)(hi >> 20) - 1022;
+    const uint64_t mb = (bits & 0x000fffffffffffffull) | (1022ull << 52);
+    double m;
+    memcpy(&m, &mb, sizeof m);
+    const uint32_t j = (hi >> 13) & 127u;
+    const double c = LOGTAB[2 * j], ln = LOGTAB[2 * j + 1];
+    const double r = m * c - 1.0;
+    double q = fma(r, 0x1.2492492492492p-3, -0x1.5555555555555p-3); /* 1/7, -1/6 */
+    q = fma(r, q, 0x1.999999999999ap-3);                               /* 1/5 */
+    q = fma(r, q, -0x1p-2);                                            /* -1/4 */
+    q = fma(r, q, 0x1.5555555555555p-2);                               /* 1/3 */
+    q = fma(r, q, -0x1p-1);                                            /* -1/2 */
+    const double l = fma(r * r, q, r);                                 /* ln(1 + r) */
+    return -fma((double)(ex - 32), 0x1.62e42fefa39efp-1, ln + l);
 }
 
 /* ------------------------------------------------------------ word stream */

@@ -5,8 +5,9 @@ The reference (Rust; crates not vendored, no toolchain here) holds no golden vec
 run, so these fixtures are regression pins of the oracle itself:
 
   parity_cases.npz     philox-mode outputs (summaries, histogram, sha256 of the final rows) of every
-                       case in tests/cases.py. CPU tests require the oracle to reproduce them; GPU
-                       tests require the engine to reproduce them.
+                       case in tests/cases.py (row store: cases(); bin store: bin_cases()). CPU tests
+                       require the oracle to reproduce them; GPU tests require the engine to
+                       reproduce them.
   c2_compat_seed42.npz reference-semantics run (ChaCha8 streams seed*10+i, first-reaction, BTPE) of
                        the C2 shape: 65,536 replicates, pure birth + binomial to 1e4 cells, seed 42:
                        pooled copy-number histogram + per-replicate final n-/n+. The GPU KS test
@@ -26,7 +27,7 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path[:0] = [os.path.join(REPO, "ecdna-evo_amd"), os.path.join(REPO, "oracle"), os.path.dirname(HERE)]
 
 import oracle  # noqa: E402
-from cases import cases  # noqa: E402
+from cases import bin_cases, cases  # noqa: E402
 from ecdna_evo_amd import abi  # noqa: E402
 
 
@@ -55,7 +56,7 @@ def c2_spec():
 
 def make_parity():
     out = {}
-    for name, spec in sorted(cases().items()):
+    for name, spec in sorted({**cases(), **bin_cases()}.items()):
         r = oracle.run(spec, mode="philox", want_rows=True)
         out[f"{name}__summaries"] = r.summaries
         out[f"{name}__hist"] = r.hist

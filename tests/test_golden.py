@@ -4,10 +4,10 @@ import os
 import numpy as np
 import pytest
 
-from cases import cases
+from cases import bin_cases, cases
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-CASES = cases()
+CASES = {**cases(), **bin_cases()}
 
 
 @pytest.fixture(scope="module")

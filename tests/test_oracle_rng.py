@@ -6,6 +6,7 @@ the reference's ChaCha8Rng is the same block function with 8 rounds (rand_chacha
 Cargo.lock:813-821). rand/rand_distr samplers: checked against their target laws.
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -146,3 +147,23 @@ def test_binomial_half_law(oracle_mod, n):
     keep = exp > 5
     chi = ((obs[keep] - exp[keep]) ** 2 / exp[keep]).sum()
     assert stats.chi2.sf(chi, keep.sum() - 1) > 1e-4, (n, chi)
+
+
+def test_log_tables_match_generator():
+    """The exponential draw's log table (draw mapping v2) is the generator's output, identical in the
+    product (ecdna-evo_amd/csrc/ssa_logtab.h) and in the oracle (oracle/ssa_logtab.h)."""
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(repo, "tools", "gen_logtab.py"), "--check"],
+                         capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+
+
+def test_softlog_near_one_keeps_relative_accuracy(oracle_mod):
+    """u -> 1 (w near 2^32): -ln u is tiny; the j = 127 table entry {1, 0} avoids cancellation."""
+    for w in range(2**32 - 2000, 2**32, 7):
+        want = -math.log1p(-(2**32 - w - 0.5) / 2**32)
+        got = oracle_mod.softlog_neg(w)
+        assert abs(got - want) <= 1e-13 * want, (w, got, want)
