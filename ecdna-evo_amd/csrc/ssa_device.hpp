@@ -73,10 +73,14 @@ __device__ __forceinline__ void stage_logtab(double2* lds) {
     __syncthreads();
 }
 
-// Extra words of one event: [w2, w3, blk1.x..w, blk2.x..w, ...], blk j = Philox(e, j, rid).
-// Only the rare paths (Lemire rejection, copy numbers > 16, NoUneven redraws) go past w3.
+// Stream words of one event (draw mapping v3): [w2, w3, spare0 .. spare(nsp-1), blk1.x,
+// blk1.y, blk1.z, blk1.w, blk2.x, ...], blk j = Philox(e, j, rid). The spares are words of earlier events'
+// blocks that no draw used (at most 2, oldest first). Only the rare paths (Lemire rejection, copy
+// numbers beyond what w3 and the spares cover, NoUneven redraws) reach the Philox blocks.
+// pos = words consumed so far; w2 counts as consumed by the cell pick (pos starts at 1).
 struct WordStream {
     uint32_t w2, w3;
+    uint32_t s0, s1, nsp;
     uint32_t e, rid_lo, rid_hi, k0, k1;
     uint32_t pos;
     uint32_t blk_id;
@@ -90,7 +94,8 @@ struct WordStream {
     __device__ __forceinline__ uint32_t next() {
         const uint32_t p = pos++;
         if (p < 2) return sel(p == 0, w2, w3);
-        const uint32_t q = p - 2;
+        if (p - 2 < nsp) return sel(p == 2, s0, s1);
+        const uint32_t q = p - 2 - nsp;
         const uint32_t j = (q >> 2) + 1;
         if (j != blk_id) {
             blk = philox4x32_10(make_uint4(e, j, rid_lo, rid_hi), k0, k1);
@@ -111,5 +116,21 @@ struct WordStream {
         return c;
     }
 };
+
+// Spare words after an event that consumed `used` stream words (0 when no cell was picked): the
+// unconsumed spares (in order), then the event's unconsumed w2 / w3, keeping the first two.
+__device__ __forceinline__ void spares_update(uint32_t used, uint32_t w2, uint32_t w3, uint32_t& s0, uint32_t& s1,
+                                              uint32_t& nsp) {
+    const uint32_t took = used > 2u ? min(used - 2u, nsp) : 0u;  // spares consumed
+    uint32_t a = took == 0u ? s0 : s1;                            // the list after dropping them
+    uint32_t n = nsp - took;
+    // append the unconsumed base words: w2 (used == 0), w3 (used <= 1)
+    const uint32_t x0 = used == 0u ? w2 : w3;
+    const uint32_t nx = used == 0u ? 2u : (used == 1u ? 1u : 0u);
+    const uint32_t b = n == 0u ? (nx >= 2u ? w3 : 0u) : x0;  // second slot
+    s0 = n == 0u ? x0 : a;
+    s1 = n >= 2u ? s1 : b;
+    nsp = min(n + nx, 2u);
+}
 
 }  // namespace ecdna

@@ -60,6 +60,7 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
     uint64_t rid = 0;
     uint16_t* row = a.rows;  // (not nullptr: keeps the pointer provably global, no flat_* accesses)
     uint32_t nm = 0, np = 0, tail = 0, wb = 0;
+    uint32_t sp0 = 0, sp1 = 0, nsp = 0;  // spare stream words (draw mapping v3)
     bool tail_ok = false;  // (HBM-only variant: tail value cached; the window variant always has it)
     // cell access through the window (WIN) or straight to HBM
     auto slot = [&](uint32_t pos) -> uint16_t& { return win[WIN ? (pos & (kWin - 1)) : 0][tid]; };
@@ -162,6 +163,7 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
             t = 0.0;
             t32 = 0.f;
             e = n_pm = n_pp = n_dm = n_dp = n_un = 0;
+            nsp = 0;
             h = kFnvOffset;
             stop = 0;
             err = 0;
@@ -244,6 +246,9 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
         WordStream ws;
         ws.w2 = w.z;
         ws.w3 = w.w;
+        ws.s0 = sp0;
+        ws.s1 = sp1;
+        ws.nsp = nsp;
         ws.e = e;
         ws.rid_lo = rid_lo;
         ws.rid_hi = rid_hi;
@@ -291,6 +296,9 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
                 if (ws.pos == 1 && n <= 32u) {
                     k1v = __popc(n == 32u ? w.w : (w.w & ((1u << n) - 1u)));
                     ws.pos = 2;
+                } else if (ws.pos == 1 && n <= 64u && nsp >= 1u) {  // w3 and the first spare word
+                    k1v = __popc(w.w) + __popc(n == 64u ? sp0 : (sp0 & ((1u << (n - 32u)) - 1u)));
+                    ws.pos = 3;
                 } else {
                     k1v = ws.binomial_half(n);
                 }
@@ -356,6 +364,7 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
             }
             x |= (uint64_t)idx << 20;
         }
+        spares_update((ch & 1u) ? ws.pos : 0u, w.z, w.w, sp0, sp1, nsp);
         // increase_nminus / decrease_nminus (src/proliferation.rs:113-117, 135-139) and the counters
         nm = nm + (ch == 0u ? 1u : 0u) - (ch == 2u ? 1u : 0u);
         n_pm += ch == 0u ? 1u : 0u;
@@ -415,23 +424,23 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
     // packed counter add: bin b (0-based, copy number b + 1) / group g, by +d (d = +1, -1 or 0, as a
     // two's complement 32-bit word: a 16-bit field never borrows from its neighbour because it is >= 1
     // when decremented)
-    auto bin_word = [&](uint32_t b) -> uint32_t* {
-        const uint32_t v = C32 ? (b >> 2) : (b >> 3);
-        const uint32_t w = C32 ? (b & 3u) : ((b & 7u) >> 1);
-        return reinterpret_cast<uint32_t*>(&cnt_v[v][tid]) + w;
+    // 32-bit word index (u32 math: LDS addresses stay 32-bit) of bin b / group g in the [vector][lane]
+    // layout: vector b / kPerVec, word (b % kPerVec) / (counters per word). Indices are masked to their
+    // range (b < K, g < NG) so the vector term folds away where it is constant.
+    uint32_t* const cnt_w = reinterpret_cast<uint32_t*>(&cnt_v[0][0]);
+    uint32_t* const sum_w = reinterpret_cast<uint32_t*>(&sum_v[0][0]);
+    const uint32_t lane4 = tid * 4u;
+    auto word_index = [&](uint32_t b) -> uint32_t {
+        return C32 ? (b >> 2) * (BLK * 4u) + lane4 + (b & 3u) : (b >> 3) * (BLK * 4u) + lane4 + ((b >> 1) & 3u);
     };
-    auto group_word = [&](uint32_t g) -> uint32_t* {
-        const uint32_t v = C32 ? (g >> 2) : (g >> 3);
-        const uint32_t w = C32 ? (g & 3u) : ((g & 7u) >> 1);
-        return reinterpret_cast<uint32_t*>(&sum_v[v][tid]) + w;
-    };
+    auto bin_word = [&](uint32_t b) -> uint32_t* { return cnt_w + word_index(b); };
     auto shifted = [&](uint32_t idx, uint32_t d) -> uint32_t { return C32 ? d : (d << ((idx & 1u) * 16)); };
     // bin of copy number k (1..K) += d (d in {1, 0xffffffff, 0}); unconditional LDS atomics, so lanes
     // with nothing to change add 0 instead of branching
     auto bin_add = [&](uint32_t k, uint32_t d) {
-        const uint32_t b = k - 1, g = b >> 3;
-        atomicAdd(bin_word(b), shifted(b, d));
-        atomicAdd(group_word(g), shifted(g, d));
+        const uint32_t b = (k - 1u) & (K - 1u), g = (b >> 3) & (uint32_t)(NG - 1);
+        atomicAdd(cnt_w + word_index(b), shifted(b, d));
+        atomicAdd(sum_w + word_index(g), shifted(g, d));
     };
     // canonical position i -> copy number, valid for i < ns (other lanes get an unused in-range value)
     auto bin_find = [&](uint32_t i) -> uint32_t {
@@ -487,6 +496,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
     uint64_t rid = 0;
     uint16_t* row = a.rows;
     uint32_t nm = 0, ns = 0, nb = 0;
+    uint32_t sp0 = 0, sp1 = 0, nsp = 0;                 // spare stream words (draw mapping v3)
     double rb0 = 0.0, rb1 = 0.0, rd0 = 0.0, rd1 = 0.0;  // the f32 rates, widened once per replicate
     double t = 0.0;
     float t32 = 0.f;
@@ -551,6 +561,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             t = 0.0;
             t32 = 0.f;
             e = n_pm = n_pp = n_dm = n_dp = n_un = 0;
+            nsp = 0;
             h = kFnvOffset;
             stop = 0;
             err = 0;
@@ -615,6 +626,9 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
         WordStream ws;
         ws.w2 = w.z;
         ws.w3 = w.w;
+        ws.s0 = sp0;
+        ws.s1 = sp1;
+        ws.nsp = nsp;
         ws.e = e;
         ws.rid_lo = rid_lo;
         ws.rid_hi = rid_hi;
@@ -641,9 +655,15 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
         uint32_t un = 0;  // 0 False, 1 True, 2 TrueWithoutNMinusIncrease
         uint32_t ev_err = 0;
         if (SEG != ECDNA_SEG_DETERMINISTIC) {
-            const bool fast = ws.pos == 1 && n <= 32u;
-            k1v = __popc(w.w & (n >= 32u ? 0xffffffffu : ((1u << (n & 31u)) - 1u)));
-            if (prolif && !fast && k <= 32767u) {  // copy numbers > 16 or a rejected pick: more stream words
+            // popcount of the stream's next n bits: w3 alone (k <= 16) or w3 and the first spare (k <= 32)
+            const uint32_t nh = n - 32u;
+            const bool fast1 = ws.pos == 1 && n <= 32u;
+            const bool fast2 = ws.pos == 1 && n > 32u && n <= 64u && nsp >= 1u;
+            const bool fast = fast1 || fast2;
+            k1v = fast1 ? __popc(w.w & (n >= 32u ? 0xffffffffu : ((1u << (n & 31u)) - 1u)))
+                        : __popc(w.w) + __popc(sp0 & (nh >= 32u ? 0xffffffffu : ((1u << (nh & 31u)) - 1u)));
+            if (prolif && fast) ws.pos = fast1 ? 2u : 3u;
+            if (prolif && !fast && k <= 32767u) {  // larger copy numbers or a rejected pick: more stream words
                 k1v = ws.binomial_half(n);
                 if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN) {
                     uint32_t tries = 1;
@@ -658,7 +678,6 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                 }
             } else if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN && prolif) {
                 uint32_t tries = 1;
-                ws.pos = 2;
                 while (k1v == 0u || k1v == n) {
                     if (tries == kNoUnevenMaxTries) {
                         ev_err = ECDNA_REP_ERR_REJECTION;
@@ -717,6 +736,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                 nb -= 1;
             }
         }
+        spares_update(nplus_ev ? ws.pos : 0u, w.z, w.w, sp0, sp1, nsp);
         nm = nm + ((ch == 0u || (prolif && un == 1u)) ? 1u : 0u) - ((BD && ch == 2u) ? 1u : 0u);
         n_un += (prolif && un != 0u) ? 1u : 0u;
         n_pm += ch == 0u ? 1u : 0u;
@@ -809,7 +829,8 @@ __global__ void __launch_bounds__(kHistBlock) ssa_hist(const HistArgs a) {
                     }
                     small += cnt;
                 }
-                nrow = np - wave_sum(small);
+                small = wave_sum(small);
+                nrow = np >= small ? np - small : 0u;  // (never trust counters past the row)
             }
             for (uint32_t c = lane * 8u; c < nrow; c += 512u) {
                 const uint4 v = *reinterpret_cast<const uint4*>(row + c);

@@ -59,6 +59,13 @@ def cases():
                                   hist_bins=64, flags=H)
     c["big_copies_no_uneven"] = abi.RunSpec(seed=22, segregation=abi.SEG_BINOMIAL_NO_UNEVEN, n_replicates=24,
                                             max_cells=300, init={17: 2, 64: 1}, flags=H)
+    # copy numbers 17..48: segregation draws from w3 plus the spare words of earlier events (draw mapping
+    # v3), with birth-death and N- events refilling the spares, and NoUneven redraws on top of them
+    c["spares_mid_copies"] = abi.RunSpec(seed=51, process=abi.BIRTH_DEATH, rates=((0.8, 1.2, 0.5, 0.4),),
+                                         n_replicates=32, max_cells=900, init={20: 30, 31: 10, 33: 5, 0: 20},
+                                         hist_bins=128, flags=H)
+    c["spares_no_uneven"] = abi.RunSpec(seed=52, segregation=abi.SEG_BINOMIAL_NO_UNEVEN, n_replicates=24,
+                                        max_cells=500, init={17: 4, 24: 4, 32: 2, 1: 6}, hist_bins=128, flags=H)
     # stop reasons and errors
     c["max_iter"] = abi.RunSpec(seed=1, n_replicates=16, max_cells=10_000, max_iter=137, flags=H)
     c["max_time"] = abi.RunSpec(seed=2, n_replicates=16, max_cells=100_000, max_time=2.5, cell_cap=4096, flags=H)

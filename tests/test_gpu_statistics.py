@@ -10,6 +10,8 @@ from ecdna_evo_amd import abi
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 KS_TOL = 0.01  # north_star: KS distance < 0.01 on the final copy-number histogram
+# both cell stores: rows (u16 per cell, swap_remove order) and bins (copy-number counters in LDS)
+STORES = {"rows": 0, "bins": abi.FLAG_BIN_STORE}
 
 
 def _ks(h1, h2):
@@ -81,11 +83,12 @@ def c5_shard_spec(rank=0, gpus=8, **kw):
 
 
 @pytest.mark.gpu
-def test_c2_ks_against_reference_semantics(engine_mod):
+@pytest.mark.parametrize("store", sorted(STORES))
+def test_c2_ks_against_reference_semantics(engine_mod, store):
     """C2 shape (65,536 replicates, pure birth + binomial to 1e4 cells, seed 42) on the GPU vs the
     committed reference-semantics fixture (ChaCha8 + first-reaction + BTPE, tests/golden/)."""
     g = np.load(os.path.join(GOLDEN, "c2_compat_seed42.npz"))
-    r = engine_mod.run(c2_spec())
+    r = engine_mod.run(c2_spec(flags=STORES[store]))
     _invariants(r, c2_spec())
     _balance(r, 1)
     ks = _ks(r.hist[0], g["hist"])
@@ -99,8 +102,9 @@ def test_c2_ks_against_reference_semantics(engine_mod):
 
 
 @pytest.mark.gpu
-def test_c2_pure_birth_exact_event_counts(engine_mod):
-    r = engine_mod.run(c2_spec())
+@pytest.mark.parametrize("store", sorted(STORES))
+def test_c2_pure_birth_exact_event_counts(engine_mod, store):
+    r = engine_mod.run(c2_spec(flags=STORES[store]))
     s = r.summaries
     full = s["stop_reason"] == abi.STOP_MAX_CELLS
     assert full.mean() > 0.99
@@ -109,15 +113,17 @@ def test_c2_pure_birth_exact_event_counts(engine_mod):
 
 
 @pytest.mark.gpu
-def test_c3_full_size_properties_and_shard_identity(engine_mod):
+@pytest.mark.parametrize("store", sorted(STORES))
+def test_c3_full_size_properties_and_shard_identity(engine_mod, store):
     """C3 at 2^20 replicates: invariants, and the two halves run as separate shards (global ids)
     reproduce the full run's summaries and histogram bit for bit (the 1-GPU == N-GPU identity)."""
-    full = engine_mod.run(c3_spec())
+    fl = STORES[store]
+    full = engine_mod.run(c3_spec(flags=fl))
     _invariants(full, c3_spec())
     _balance(full, 1)
     half = 1 << 19
-    a = engine_mod.run(c3_spec(0, half))
-    b = engine_mod.run(c3_spec(half, half))
+    a = engine_mod.run(c3_spec(0, half, flags=fl))
+    b = engine_mod.run(c3_spec(half, half, flags=fl))
     for f in full.summaries.dtype.names:
         np.testing.assert_array_equal(np.concatenate([a.summaries[f], b.summaries[f]]), full.summaries[f])
     np.testing.assert_array_equal(a.hist + b.hist, full.hist)
@@ -128,9 +134,10 @@ def test_c3_full_size_properties_and_shard_identity(engine_mod):
 
 
 @pytest.mark.gpu
-def test_c3_matches_oracle_on_a_sample(engine_mod, oracle_mod):
+@pytest.mark.parametrize("store", sorted(STORES))
+def test_c3_matches_oracle_on_a_sample(engine_mod, oracle_mod, store):
     """Replicates 0..4095 of the C3 run, checked against the oracle bit for bit (hash on)."""
-    spec = c3_spec(0, 4096, flags=abi.FLAG_EVENT_HASH)
+    spec = c3_spec(0, 4096, flags=abi.FLAG_EVENT_HASH | STORES[store])
     g = engine_mod.run(spec)
     c = oracle_mod.run(spec, mode="philox")
     for f in g.summaries.dtype.names:
@@ -142,10 +149,10 @@ def test_c3_matches_oracle_on_a_sample(engine_mod, oracle_mod):
 def test_engine_reproduces_parity_fixture(engine_mod):
     """The GPU reproduces the committed oracle fixtures without running the oracle."""
     import make_golden
-    from cases import cases
+    from cases import bin_cases, cases
 
     fx = np.load(os.path.join(GOLDEN, "parity_cases.npz"))
-    for name, spec in sorted(cases().items()):
+    for name, spec in sorted({**cases(), **bin_cases()}.items()):
         r = engine_mod.run(spec, want_rows=True)
         want = fx[f"{name}__summaries"]
         for f in want.dtype.names:
@@ -177,33 +184,54 @@ def test_abc_sweep_shape_small(engine_mod, oracle_mod):
 
 
 @pytest.mark.gpu
-def test_c4_shard_full_size_properties(engine_mod, oracle_mod):
+@pytest.mark.parametrize("store", sorted(STORES))
+def test_c4_shard_full_size_properties(engine_mod, oracle_mod, store):
     """C4 rank-0 shard at full size (524,288 replicates, 128 parameter sets with per-set rates and
     initial copy numbers): invariants, bookkeeping, per-set replicate counts, and 256 replicates of a
     birth-death set with initial k = 1 against the oracle bit for bit (event hash)."""
-    spec = c4_shard_spec(flags=abi.FLAG_EVENT_HASH)
+    spec = c4_shard_spec(flags=abi.FLAG_EVENT_HASH | STORES[store])
     r = engine_mod.run(spec)
     _invariants(r, spec)
     _balance(r, 1)
     assert np.all(r.totals["replicates"][:128] == 4096) and np.all(r.totals["replicates"][128:] == 0)
     first = 37 * 4096  # set 37: b1 = 1.2, d = 0.2, k0 = 1
-    c = oracle_mod.run(c4_shard_spec(first_replicate=first, n_replicates=256, flags=abi.FLAG_EVENT_HASH),
-                       mode="philox")
+    c = oracle_mod.run(c4_shard_spec(first_replicate=first, n_replicates=256,
+                                     flags=abi.FLAG_EVENT_HASH | STORES[store]), mode="philox")
     for f in c.summaries.dtype.names:
         np.testing.assert_array_equal(r.summaries[f][first:first + 256], c.summaries[f], err_msg=f)
 
 
 @pytest.mark.gpu
-def test_c5_shard_full_size_properties(engine_mod, oracle_mod):
+@pytest.mark.parametrize("store", sorted(STORES))
+def test_c5_shard_full_size_properties(engine_mod, oracle_mod, store):
     """C5 rank-0 shard at full size (32,768 replicates, rows up to 1e6 cells = 2 MB, 65 GB of rows):
     invariants, bookkeeping, the stop law of a critical-ish turnover process, and replicates 0..3
-    (about 2e7 events each) against the oracle bit for bit (event hash)."""
-    spec = c5_shard_spec(flags=abi.FLAG_EVENT_HASH)
+    (about 2e7 events each) against the oracle bit for bit (event hash). The bin store runs its
+    256-bin, u32-counter variant here (cell_cap 1e6 > 65535)."""
+    kw = dict(flags=abi.FLAG_EVENT_HASH | STORES[store], bin_kmax=256 if store == "bins" else 0)
+    spec = c5_shard_spec(**kw)
     r = engine_mod.run(spec)
     _invariants(r, spec)
     _balance(r, 1000)
     stops = set(r.summaries["stop_reason"].tolist())
     assert stops <= {abi.STOP_MAX_CELLS, abi.STOP_MAX_TIME, abi.STOP_ABSORBING}, stops
-    c = oracle_mod.run(c5_shard_spec(n_replicates=4, flags=abi.FLAG_EVENT_HASH), mode="philox", n_threads=4)
+    c = oracle_mod.run(c5_shard_spec(n_replicates=4, **kw), mode="philox", n_threads=4)
     for f in c.summaries.dtype.names:
         np.testing.assert_array_equal(r.summaries[f][:4], c.summaries[f], err_msg=f)
+
+
+@pytest.mark.gpu
+def test_c3_bin_store_and_row_store_agree_in_law(engine_mod):
+    """The two cell stores simulate the same process (a uniform cell pick is invariant under the
+    arrangement of the cells): at C3 size their pooled copy-number histograms are
+    within the north-star KS tolerance and per-replicate laws (final size, N- fraction, events) agree."""
+    from scipy import stats
+
+    a = engine_mod.run(c3_spec(n=1 << 18))
+    b = engine_mod.run(c3_spec(n=1 << 18, flags=abi.FLAG_BIN_STORE, seed=4242))
+    assert _ks(a.hist[0], b.hist[0]) < KS_TOL
+    for f in ("iters", "nplus", "nminus"):
+        assert stats.ks_2samp(a.summaries[f], b.summaries[f]).pvalue > 1e-4, f
+    ma = (np.arange(1025) * a.hist[0]).sum() / a.hist[0].sum()
+    mb = (np.arange(1025) * b.hist[0]).sum() / b.hist[0].sum()
+    assert abs(ma - mb) / ma < 0.01
