@@ -7,7 +7,8 @@
 //
 // Additions: --gpus N (replicate shards on N devices, one host thread each), --time {f32,f64}
 // (default f32 = the reference's process.time), --cell-cap (row capacity; needed with --years),
-// --hist-bins, --dry-run (print the resolved options as JSON and exit).
+// --hist-bins, --dry-run (print the resolved options as JSON and exit), --cell-store {bins,rows}
+// (default bins: copy-number counters in LDS) and --bin-kmax {64,256}.
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -55,6 +56,8 @@ struct Options {
     uint64_t cell_cap = 0;
     uint32_t hist_bins = 1025;
     bool dry_run = false;
+    bool rows = false;       // --cell-store rows
+    uint32_t bin_kmax = 64;  // --bin-kmax
 };
 
 [[noreturn]] void usage_error(const std::string& msg) {
@@ -91,6 +94,8 @@ void print_help() {
         "      --cell-cap <CELLS>           N+ row capacity [default: cells, or 2^24 with --years]\n"
         "      --hist-bins <BINS>           [default: 1025]\n"
         "      --dry-run                    print the resolved options as JSON and exit\n"
+        "      --cell-store <bins|rows>     N+ cell store of the engine [default: bins]\n"
+        "      --bin-kmax <64|256>          copy numbers held as counters by the bin store [default: 64]\n"
         "  -h, --help                       Print help\n");
 }
 
@@ -205,6 +210,14 @@ Options parse(int argc, char** argv) {
             o.hist_bins = (uint32_t)parse_u64(a, need(a));
         } else if (a == "--dry-run") {
             o.dry_run = true;
+        } else if (a == "--cell-store") {
+            const std::string v = need(a);
+            if (v != "bins" && v != "rows") usage_error("--cell-store must be bins or rows");
+            o.rows = v == "rows";
+        } else if (a == "--bin-kmax") {
+            const uint64_t v = parse_u64(a, need(a));
+            if (v != 64 && v != 256) usage_error("--bin-kmax must be 64 or 256");
+            o.bin_kmax = (uint32_t)v;
         } else if (!a.empty() && a[0] == '-') {
             usage_error("unexpected argument '" + a + "' found");
         } else {
@@ -354,13 +367,14 @@ int main(int argc, char** argv) {
             "{\"process\":\"%s\",\"segregation\":\"%s\",\"b0\":%.9g,\"b1\":%.9g,\"d0\":%.9g,\"d1\":%.9g,\"cells\":%llu,"
             "\"years\":%llu,\"runs\":%llu,\"seed\":%llu,\"verbosity\":%d,\"parallel\":%s,\"snapshots\":%s,"
             "\"subsamples\":%s,\"initial\":%s,\"cell_cap\":%llu,\"first_idx\":%llu,\"max_iter\":%llu,"
-            "\"time\":\"%s\",\"gpus\":%d}\n",
+            "\"time\":\"%s\",\"gpus\":%d,\"cell_store\":\"%s\",\"bin_kmax\":%u}\n",
             r.birth_death ? "BirthDeath" : "PureBirth", o.segregation_name.c_str(), (double)o.b0, (double)o.b1,
             (double)r.d0, (double)r.d1, (unsigned long long)r.cells,
             (unsigned long long)years_cap, (unsigned long long)r.runs, (unsigned long long)o.seed, r.verbosity,
             r.parallel ? "true" : "false", json_list(r.snapshots).c_str(), json_list(o.subsamples).c_str(),
             ecdna::host::to_json(r.initial).c_str(), (unsigned long long)r.cell_cap,
-            (unsigned long long)(o.seed * 10), (unsigned long long)kMaxIter, o.time_f64 ? "f64" : "f32", o.gpus);
+            (unsigned long long)(o.seed * 10), (unsigned long long)kMaxIter, o.time_f64 ? "f64" : "f32", o.gpus,
+            o.rows ? "rows" : "bins", o.bin_kmax);
         return 0;
     }
 
@@ -382,7 +396,8 @@ int main(int argc, char** argv) {
     p.max_time = (double)(float)years_cap;  // `years as f32`, src/clap_app.rs:205
     p.max_iter = kMaxIter;
     p.cell_cap = (uint32_t)std::min<uint64_t>(r.cell_cap, 0xffffffffull);
-    p.flags = (o.time_f64 ? 0u : ECDNA_FLAG_TIME_F32) | ECDNA_FLAG_SNAPSHOT_ROWS;
+    p.flags = (o.time_f64 ? 0u : ECDNA_FLAG_TIME_F32) | ECDNA_FLAG_SNAPSHOT_ROWS | (o.rows ? 0u : ECDNA_FLAG_BIN_STORE);
+    p.bin_kmax = o.rows ? 0u : o.bin_kmax;
     p.init_copies = r.initial.nplus.empty() ? nullptr : r.initial.nplus.data();
     p.init_nplus = (uint32_t)r.initial.nplus.size();
     p.init_nminus = r.initial.nminus;

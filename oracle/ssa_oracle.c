@@ -103,12 +103,17 @@ double oracle_softlog_neg(uint32_t w) {
 
 /* ------------------------------------------------------------ word stream */
 
-/* Per-event extra words: [w2, w3, blk1.x, blk1.y, blk1.z, blk1.w, blk2.x, ...]
- * where blk j = Philox(ctr = (e, j, rid lo, rid hi)). */
+/* Per-event stream words (draw mapping v3): [w2, w3, spare[0], .., spare[nsp-1], blk1.x, blk1.y, blk1.z,
+ * blk1.w, blk2.x, ...] where blk j = Philox(ctr = (e, j, rid lo, rid hi)) and the spares are words of
+ * earlier events' blocks that no draw consumed (at most 2, oldest first; spares_update()). Each word
+ * is used at most once and whether it is used depends only on draws already made, so every draw
+ * stays an independent uniform. pos = words consumed. */
 typedef struct {
     uint32_t key[2];
     uint32_t e, rid_lo, rid_hi;
     uint32_t w2, w3;
+    uint32_t sp[2];
+    uint32_t nsp;
     uint32_t buf[4];
     uint32_t blk;
     uint32_t pos;
@@ -118,7 +123,8 @@ static uint32_t ws_next(wstream* s) {
     uint32_t p = s->pos++;
     if (p == 0) return s->w2;
     if (p == 1) return s->w3;
-    uint32_t q = p - 2;
+    if (p - 2 < s->nsp) return s->sp[p - 2];
+    uint32_t q = p - 2 - s->nsp;
     uint32_t j = q / 4 + 1;
     if (j != s->blk) {
         uint32_t ctr[4] = {s->e, j, s->rid_lo, s->rid_hi};
@@ -193,6 +199,20 @@ static int segregate(wstream* s, int seg, uint32_t n, uint32_t* k1, int* uneven)
     return -1;
 }
 
+/* After an event that consumed `used` stream words: spares = (the unconsumed spares, in order) followed by
+ * the event's unconsumed base words (w2 if used == 0, then w3 if used <= 1), truncated to the first two. */
+static void spares_update(uint32_t sp[2], uint32_t* nsp, uint32_t used, uint32_t w2, uint32_t w3) {
+    uint32_t took = used > 2 ? used - 2 : 0;
+    if (took > *nsp) took = *nsp;
+    uint32_t list[4], n = 0;
+    for (uint32_t i = took; i < *nsp; ++i) list[n++] = sp[i];
+    if (used == 0) list[n++] = w2;
+    if (used <= 1) list[n++] = w3;
+    if (n > 2) n = 2;
+    for (uint32_t i = 0; i < n; ++i) sp[i] = list[i];
+    *nsp = n;
+}
+
 static void ws_init(wstream* s, uint64_t seed, uint64_t rid, uint32_t e, uint32_t w2, uint32_t w3) {
     s->key[0] = (uint32_t)seed;
     s->key[1] = (uint32_t)(seed >> 32);
@@ -201,6 +221,7 @@ static void ws_init(wstream* s, uint64_t seed, uint64_t rid, uint32_t e, uint32_
     s->rid_hi = (uint32_t)(rid >> 32);
     s->w2 = w2;
     s->w3 = w3;
+    s->nsp = 0;
     s->blk = 0;
     s->pos = 0;
 }
@@ -435,6 +456,7 @@ static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16
                                ecdna_rep_summary_t* out, ecdna_snapshot_t* snap_meta, uint16_t* snap_rows,
                                uint64_t snap_stride) {
     uint32_t sj = 0;
+    uint32_t spare[2] = {0, 0}, nspare = 0; /* spare stream words (draw mapping v3) */
     const uint64_t set = rid / p->reps_per_set;
     const ecdna_rates_t rt = p->rates[set];
     const int bd = p->process == ECDNA_BIRTH_DEATH;
@@ -515,6 +537,9 @@ static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16
         double tau = oracle_softlog_neg(w[0]) / a0;
         wstream ws;
         ws_init(&ws, p->seed, rid, e, w[2], w[3]);
+        ws.sp[0] = spare[0];
+        ws.sp[1] = spare[1];
+        ws.nsp = nspare;
         uint64_t x = (uint64_t)ch;
         switch (ch) {
             case ECDNA_EV_PROLIF_NMINUS: /* increase_nminus (src/proliferation.rs:113-117) */
@@ -554,6 +579,7 @@ static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16
                 break;
             }
         }
+        spares_update(spare, &nspare, (ch & 1) ? ws.pos : 0u, w[2], w[3]);
         cnt[ch] += 1;
         e += 1;
         if (f32t)

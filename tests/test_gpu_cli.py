@@ -74,16 +74,19 @@ CASES = {
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("store", ["bins", "rows"])
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_cli_writes_what_the_reference_writes(name, engine_mod, oracle_mod, tmp_path):
+def test_cli_writes_what_the_reference_writes(name, store, engine_mod, oracle_mod, tmp_path):
     args, c = CASES[name]
-    out = subprocess.run([CLI, *args, str(tmp_path)], capture_output=True, text=True, timeout=300)
+    out = subprocess.run([CLI, *args, "--cell-store", store, str(tmp_path)], capture_output=True, text=True,
+                         timeout=300)
     assert out.returncode == 0, out.stderr
     runs = int(args[args.index("--runs") + 1])
     seed = int(args[args.index("--seed") + 1])
     snaps = c.get("snaps") or abi.default_snapshots(c["cells"])
     spec = abi.RunSpec(process=c["process"], rates=(c["rates"],), seed=seed, n_replicates=runs, max_cells=c["cells"],
-                       snapshots=snaps, flags=abi.FLAG_TIME_F32 | abi.FLAG_SNAPSHOT_ROWS)
+                       snapshots=snaps, bin_kmax=64 if store == "bins" else 0,
+                       flags=abi.FLAG_TIME_F32 | abi.FLAG_SNAPSHOT_ROWS | (abi.FLAG_BIN_STORE if store == "bins" else 0))
     res = oracle_mod.run(spec, mode="philox", want_rows=True)
     want = expected_files(spec, res, c["rates"], c["subs"])
     got = written_files(tmp_path)

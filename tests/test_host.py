@@ -209,3 +209,14 @@ def test_subsample_is_uniform_without_replacement(host):
         nm_total += onm.value
     # each of the 50 cells is kept with probability 10/50
     assert abs(counts[1:].mean() / 3000 - 0.2) < 0.01 and abs(nm_total / (3000 * 10) - 0.2) < 0.015
+
+
+def test_cli_cell_store_options(host):
+    d = dry()
+    assert (d["cell_store"], d["bin_kmax"]) == ("bins", 64)
+    d = dry("--cell-store", "rows")
+    assert d["cell_store"] == "rows"
+    assert dry("--bin-kmax", "256")["bin_kmax"] == 256
+    for bad in (["--cell-store", "tree"], ["--bin-kmax", "100"]):
+        out = subprocess.run([CLI, "--dry-run", *bad, "/tmp/ecdna_out"], capture_output=True, text=True)
+        assert out.returncode != 0
