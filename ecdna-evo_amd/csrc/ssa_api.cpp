@@ -374,7 +374,7 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
     if (c->bin_k) {
         // bin store: LDS-resident events, bounded by issue and LDS latency: every resident block helps
         CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per_cu, ecdna::bin_stepper_kernel(p->process, p->segregation, c->bin_k, c->bin_c32),
+            &per_cu, ecdna::bin_stepper_kernel(p->process, p->segregation, c->bin_k, c->bin_c32, p->flags),
             (int)c->stepper_block, 0));
     } else {
         CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(

@@ -408,7 +408,7 @@ __device__ __forceinline__ uint32_t vec_get(const uint4& v, int j) {
     return (w[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
 }
 
-template <bool BD, int SEG, int NG, bool C32, int BLK>
+template <bool BD, int SEG, int NG, bool C32, int BLK, int TF>
 __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
     using L = BinLayout<NG, C32>;
     constexpr uint32_t K = L::kK;
@@ -418,8 +418,6 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
     stage_logtab(logtab);
     const uint32_t tid = threadIdx.x;
     const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
-    const bool f32t = (a.flags & ECDNA_FLAG_TIME_F32) != 0;
-    const bool hash_on = (a.flags & ECDNA_FLAG_EVENT_HASH) != 0;
 
     // packed counter add: bin b (0-based, copy number b + 1) / group g, by +d (d = +1, -1 or 0, as a
     // two's complement 32-bit word: a 16-bit field never borrows from its neighbour because it is >= 1
@@ -491,6 +489,10 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
         for (uint32_t j = 0; j < nb; ++j) dst[pos + j] = big[j];
     };
 
+    // TF: 0 = f64 time and no event hash (compile-time), 1 = both from the runtime flags
+    const bool f32t = TF ? (a.flags & ECDNA_FLAG_TIME_F32) != 0 : false;
+    const bool hash_on = TF ? (a.flags & ECDNA_FLAG_EVENT_HASH) != 0 : false;
+
     bool active = false, have = false;
     uint32_t li = 0;
     uint64_t rid = 0;
@@ -548,6 +550,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             bins_zero();
             ns = 0;
             nb = 0;
+#pragma unroll 1
             for (uint32_t j = 0; j < cnt; ++j) {
                 const uint32_t kk = src[j];
                 if (kk <= K) {
@@ -570,9 +573,9 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                 err = ECDNA_REP_ERR_EMPTY;
                 stop = ECDNA_STOP_ERROR;
                 active = false;
-                continue;
             }
         }
+        if (!active) continue;  // (an empty initial distribution)
         const uint32_t np = ns + nb;
 
         // propensities rate_i * population_i over [n-, n+(, n-, n+)]
@@ -584,88 +587,97 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             cC = cB + rd0 * fm;
             a0 = cC + rd1 * fp;
         }
-        {
-            const bool t_over = f32t ? (t32 >= a.max_time32) : (t >= a.max_time);
-            uint32_t s = (a0 > 0.0) ? 0u : (uint32_t)ECDNA_STOP_ABSORBING;
-            s = t_over ? (uint32_t)ECDNA_STOP_MAX_TIME : s;
-            s = ((uint64_t)nm + np >= a.stop_cells) ? (uint32_t)ECDNA_STOP_MAX_CELLS : s;
-            s = (e >= a.max_iter) ? (uint32_t)ECDNA_STOP_MAX_ITER : s;
-            if (s) {
-                stop = s;
-                active = false;
-                continue;
+        // stop checks: one test here, the reason only when a lane stops
+        const bool t_over = f32t ? (t32 >= a.max_time32) : (t >= a.max_time);
+        const bool cells_over = (uint64_t)nm + np >= a.stop_cells;
+        if ((e >= a.max_iter) || cells_over || t_over || !(a0 > 0.0)) {
+            stop = (e >= a.max_iter) ? (uint32_t)ECDNA_STOP_MAX_ITER
+                   : cells_over     ? (uint32_t)ECDNA_STOP_MAX_CELLS
+                   : t_over         ? (uint32_t)ECDNA_STOP_MAX_TIME
+                                    : (uint32_t)ECDNA_STOP_ABSORBING;
+            active = false;
+        } else {
+            if (a.n_snap) {  // src/process.rs:122-145, as in ssa_stepper
+                const uint64_t total = (uint64_t)nm + np;
+                while (sj < a.n_snap) {
+                    bool any = false;
+                    for (uint32_t q = 0; q < a.n_snap; ++q) any |= (q >= sj) && (a.snap_cells[q] == total);
+                    if (!any) break;
+                    ecdna_snapshot_t* m = a.snap_meta + (uint64_t)li * a.n_snap + sj;
+                    m->time = f32t ? (double)t32 : t;
+                    m->nminus = nm;
+                    m->nplus = np;
+                    m->taken = 1u;
+                    m->reserved = 0u;
+                    if (a.snap_rows) expand(a.snap_rows + ((uint64_t)li * a.n_snap + sj) * a.row_stride, row, nb);
+                    ++sj;
+                }
             }
-        }
-        if (a.n_snap) {  // src/process.rs:122-145, as in ssa_stepper
-            const uint64_t total = (uint64_t)nm + np;
-            while (sj < a.n_snap) {
-                bool any = false;
-                for (uint32_t q = 0; q < a.n_snap; ++q) any |= (q >= sj) && (a.snap_cells[q] == total);
-                if (!any) break;
-                ecdna_snapshot_t* m = a.snap_meta + (uint64_t)li * a.n_snap + sj;
-                m->time = f32t ? (double)t32 : t;
-                m->nminus = nm;
-                m->nplus = np;
-                m->taken = 1u;
-                m->reserved = 0u;
-                if (a.snap_rows) expand(a.snap_rows + ((uint64_t)li * a.n_snap + sj) * a.row_stride, row, nb);
-                ++sj;
+
+            const uint32_t rid_lo = (uint32_t)rid, rid_hi = (uint32_t)(rid >> 32);
+            const uint4 w = philox4x32_10(make_uint4(e, 0u, rid_lo, rid_hi), k0, k1);
+            // direct method: the channel is the number of cumulative propensities <= target (the first i
+            // with target < c_i; the c_i are non-decreasing)
+            const double target = (((double)w.y + 0.5) * 0x1p-32) * a0;
+            uint32_t ch = (target >= cA ? 1u : 0u);
+            if (BD) ch += (target >= cB ? 1u : 0u) + (target >= cC ? 1u : 0u);
+            const bool nplus_ev = (ch & 1u) != 0;  // ProliferateNPlus or DeathNPlus: a cell is picked
+            const bool prolif = ch == 1u;
+
+            WordStream ws;
+            ws.w2 = w.z;
+            ws.w3 = w.w;
+            ws.s0 = sp0;
+            ws.s1 = sp1;
+            ws.nsp = nsp;
+            ws.e = e;
+            ws.rid_lo = rid_lo;
+            ws.rid_hi = rid_hi;
+            ws.k0 = k0;
+            ws.k1 = k1;
+            ws.pos = 1;
+            ws.blk_id = 0;
+            ws.blk = make_uint4(0, 0, 0, 0);
+
+            // uniform N+ cell: Lemire multiply-shift on w2; exact rejection (rare) from the stream
+            uint64_t m = (uint64_t)w.z * np;
+            if (nplus_ev && (uint32_t)m < np) {
+                const uint32_t thr = (0u - np) % np;
+                while ((uint32_t)m < thr) m = (uint64_t)ws.next() * np;
             }
-        }
+            const uint32_t idx = (uint32_t)(m >> 32);
+            const bool small = idx < ns;
+            uint32_t k = bin_find(small ? idx : 0u);
+            if (nplus_ev && !small) k = gload_u16(row + (idx - ns));  // large-k row (rare)
 
-        const uint32_t rid_lo = (uint32_t)rid, rid_hi = (uint32_t)(rid >> 32);
-        const uint4 w = philox4x32_10(make_uint4(e, 0u, rid_lo, rid_hi), k0, k1);
-        // direct method: the channel is the number of cumulative propensities <= target (the first i
-        // with target < c_i; the c_i are non-decreasing)
-        const double target = (((double)w.y + 0.5) * 0x1p-32) * a0;
-        uint32_t ch = (target >= cA ? 1u : 0u);
-        if (BD) ch += (target >= cB ? 1u : 0u) + (target >= cC ? 1u : 0u);
-        const bool nplus_ev = (ch & 1u) != 0;  // ProliferateNPlus or DeathNPlus: a cell is picked
-        const bool prolif = ch == 1u;
-
-        WordStream ws;
-        ws.w2 = w.z;
-        ws.w3 = w.w;
-        ws.s0 = sp0;
-        ws.s1 = sp1;
-        ws.nsp = nsp;
-        ws.e = e;
-        ws.rid_lo = rid_lo;
-        ws.rid_hi = rid_hi;
-        ws.k0 = k0;
-        ws.k1 = k1;
-        ws.pos = 1;
-        ws.blk_id = 0;
-        ws.blk = make_uint4(0, 0, 0, 0);
-
-        // uniform N+ cell: Lemire multiply-shift on w2; exact rejection (rare) from the stream
-        uint64_t m = (uint64_t)w.z * np;
-        if (nplus_ev && (uint32_t)m < np) {
-            const uint32_t thr = (0u - np) % np;
-            while ((uint32_t)m < thr) m = (uint64_t)ws.next() * np;
-        }
-        const uint32_t idx = (uint32_t)(m >> 32);
-        const bool small = idx < ns;
-        uint32_t k = bin_find(small ? idx : 0u);
-        if (nplus_ev && !small) k = gload_u16(row + (idx - ns));  // large-k row (rare)
-
-        // Exponential::increase_nplus (src/proliferation.rs:25-111): its draws and error checks
-        const uint32_t n = 2u * k;
-        uint32_t k1v = k;
-        uint32_t un = 0;  // 0 False, 1 True, 2 TrueWithoutNMinusIncrease
-        uint32_t ev_err = 0;
-        if (SEG != ECDNA_SEG_DETERMINISTIC) {
-            // popcount of the stream's next n bits: w3 alone (k <= 16) or w3 and the first spare (k <= 32)
-            const uint32_t nh = n - 32u;
-            const bool fast1 = ws.pos == 1 && n <= 32u;
-            const bool fast2 = ws.pos == 1 && n > 32u && n <= 64u && nsp >= 1u;
-            const bool fast = fast1 || fast2;
-            k1v = fast1 ? __popc(w.w & (n >= 32u ? 0xffffffffu : ((1u << (n & 31u)) - 1u)))
-                        : __popc(w.w) + __popc(sp0 & (nh >= 32u ? 0xffffffffu : ((1u << (nh & 31u)) - 1u)));
-            if (prolif && fast) ws.pos = fast1 ? 2u : 3u;
-            if (prolif && !fast && k <= 32767u) {  // larger copy numbers or a rejected pick: more stream words
-                k1v = ws.binomial_half(n);
-                if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN) {
+            // Exponential::increase_nplus (src/proliferation.rs:25-111): its draws and error checks
+            const uint32_t n = 2u * k;
+            uint32_t k1v = k;
+            uint32_t un = 0;  // 0 False, 1 True, 2 TrueWithoutNMinusIncrease
+            uint32_t ev_err = 0;
+            if (SEG != ECDNA_SEG_DETERMINISTIC) {
+                // popcount of the stream's next n bits: w3 alone (k <= 16) or w3 and the first spare (k <= 32)
+                const uint32_t nh = n - 32u;
+                const bool fast1 = ws.pos == 1 && n <= 32u;
+                const bool fast2 = ws.pos == 1 && n > 32u && n <= 64u && nsp >= 1u;
+                const bool fast = fast1 || fast2;
+                k1v = fast1 ? __popc(w.w & (n >= 32u ? 0xffffffffu : ((1u << (n & 31u)) - 1u)))
+                            : __popc(w.w) + __popc(sp0 & (nh >= 32u ? 0xffffffffu : ((1u << (nh & 31u)) - 1u)));
+                if (prolif && fast) ws.pos = fast1 ? 2u : 3u;
+                if (prolif && !fast && k <= 32767u) {  // larger copy numbers or a rejected pick: more words
+                    k1v = ws.binomial_half(n);
+                    if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN) {
+                        uint32_t tries = 1;
+                        while (k1v == 0u || k1v == n) {
+                            if (tries == kNoUnevenMaxTries) {
+                                ev_err = ECDNA_REP_ERR_REJECTION;
+                                break;
+                            }
+                            k1v = ws.binomial_half(n);
+                            ++tries;
+                        }
+                    }
+                } else if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN && prolif) {
                     uint32_t tries = 1;
                     while (k1v == 0u || k1v == n) {
                         if (tries == kNoUnevenMaxTries) {
@@ -676,82 +688,71 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                         ++tries;
                     }
                 }
-            } else if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN && prolif) {
-                uint32_t tries = 1;
-                while (k1v == 0u || k1v == n) {
-                    if (tries == kNoUnevenMaxTries) {
-                        ev_err = ECDNA_REP_ERR_REJECTION;
-                        break;
+                if (SEG != ECDNA_SEG_BINOMIAL_NO_UNEVEN)
+                    un = (k1v == 0u || k1v == n) ? (SEG == ECDNA_SEG_BINOMIAL_NO_NMINUS ? 2u : 1u) : 0u;
+            }
+            // checked_mul panic (src/proliferation.rs:63-67), then the row-capacity check
+            ev_err = (k > 32767u) ? (uint32_t)ECDNA_REP_ERR_OVERFLOW : ev_err;
+            ev_err = (ev_err == 0u && un == 0u && np + 1u > a.cell_cap) ? (uint32_t)ECDNA_REP_ERR_CELL_CAP : ev_err;
+            if (prolif && ev_err) {  // the event is not applied; the replicate stops (rare)
+                err = ev_err;
+                stop = ECDNA_STOP_ERROR;
+                active = false;
+            } else {
+                const double tau = softlog_neg(w.x, logtab) / a0;
+
+                // daughters (none for a death): [k1, k2] on an even split, [n] on an uneven one
+                const uint32_t da = (un == 0u) ? k1v : n;
+                const uint32_t db = n - k1v;
+                const bool has_a = prolif, has_b = prolif && un == 0u;
+                const bool sa = has_a && da <= K, sb = has_b && db <= K;
+                const uint32_t ns_old = ns;
+                // common case: every copy number involved is binned -> LDS only, no branch
+                bin_add(small ? k : 1u, (nplus_ev && small) ? 0xffffffffu : 0u);
+                bin_add(sa ? da : 1u, sa ? 1u : 0u);
+                bin_add(sb ? db : 1u, sb ? 1u : 0u);
+                ns = ns - ((nplus_ev && small) ? 1u : 0u) + (sa ? 1u : 0u) + (sb ? 1u : 0u);
+                if (nplus_ev && (!small || (has_a && !sa) || (has_b && !sb))) {  // the large-k row (rare)
+                    uint32_t open = small ? 0xffffffffu : idx - ns_old;  // B slot freed by a large picked cell
+                    if (has_a && !sa) {
+                        if (open != 0xffffffffu) {
+                            row[open] = (uint16_t)da;
+                            open = 0xffffffffu;
+                        } else {
+                            row[nb++] = (uint16_t)da;
+                        }
                     }
-                    k1v = ws.binomial_half(n);
-                    ++tries;
+                    if (has_b && !sb) {
+                        if (open != 0xffffffffu) {
+                            row[open] = (uint16_t)db;
+                            open = 0xffffffffu;
+                        } else {
+                            row[nb++] = (uint16_t)db;
+                        }
+                    }
+                    if (open != 0xffffffffu) {  // swap_remove(open) from B
+                        if (open != nb - 1) row[open] = (uint16_t)gload_u16(row + nb - 1);
+                        nb -= 1;
+                    }
+                }
+                spares_update(nplus_ev ? ws.pos : 0u, w.z, w.w, sp0, sp1, nsp);
+                nm = nm + ((ch == 0u || (prolif && un == 1u)) ? 1u : 0u) - ((BD && ch == 2u) ? 1u : 0u);
+                n_un += (prolif && un != 0u) ? 1u : 0u;
+                n_pm += ch == 0u ? 1u : 0u;
+                n_pp += ch == 1u ? 1u : 0u;
+                n_dm += ch == 2u ? 1u : 0u;
+                n_dp += ch == 3u ? 1u : 0u;
+                e += 1;
+                if (f32t)
+                    t32 = t32 + (float)tau;
+                else
+                    t = t + tau;
+                if (hash_on) {
+                    const uint64_t x = (uint64_t)ch | (prolif ? ((uint64_t)k1v << 2) : 0ull) |
+                                       (nplus_ev ? ((uint64_t)idx << 20) : 0ull);
+                    h = (h ^ x) * kFnvPrime;
                 }
             }
-            if (SEG != ECDNA_SEG_BINOMIAL_NO_UNEVEN)
-                un = (k1v == 0u || k1v == n) ? (SEG == ECDNA_SEG_BINOMIAL_NO_NMINUS ? 2u : 1u) : 0u;
-        }
-        // checked_mul panic (src/proliferation.rs:63-67), then the row-capacity check
-        ev_err = (k > 32767u) ? (uint32_t)ECDNA_REP_ERR_OVERFLOW : ev_err;
-        ev_err = (ev_err == 0u && un == 0u && np + 1u > a.cell_cap) ? (uint32_t)ECDNA_REP_ERR_CELL_CAP : ev_err;
-        if (prolif && ev_err) {
-            err = ev_err;
-            stop = ECDNA_STOP_ERROR;
-            active = false;
-            continue;
-        }
-
-        const double tau = softlog_neg(w.x, logtab) / a0;
-
-        // daughters (none for a death): [k1, k2] on an even split, [n] on an uneven one
-        const uint32_t da = (un == 0u) ? k1v : n;
-        const uint32_t db = n - k1v;
-        const bool has_a = prolif, has_b = prolif && un == 0u;
-        const bool sa = has_a && da <= K, sb = has_b && db <= K;
-        const uint32_t ns_old = ns;
-        // common case: every copy number involved is binned -> LDS only, no branch
-        bin_add(small ? k : 1u, (nplus_ev && small) ? 0xffffffffu : 0u);
-        bin_add(sa ? da : 1u, sa ? 1u : 0u);
-        bin_add(sb ? db : 1u, sb ? 1u : 0u);
-        ns = ns - ((nplus_ev && small) ? 1u : 0u) + (sa ? 1u : 0u) + (sb ? 1u : 0u);
-        if (nplus_ev && (!small || (has_a && !sa) || (has_b && !sb))) {  // the large-k row (rare)
-            uint32_t open = small ? 0xffffffffu : idx - ns_old;  // B slot freed by a large picked cell
-            if (has_a && !sa) {
-                if (open != 0xffffffffu) {
-                    row[open] = (uint16_t)da;
-                    open = 0xffffffffu;
-                } else {
-                    row[nb++] = (uint16_t)da;
-                }
-            }
-            if (has_b && !sb) {
-                if (open != 0xffffffffu) {
-                    row[open] = (uint16_t)db;
-                    open = 0xffffffffu;
-                } else {
-                    row[nb++] = (uint16_t)db;
-                }
-            }
-            if (open != 0xffffffffu) {  // swap_remove(open) from B
-                if (open != nb - 1) row[open] = (uint16_t)gload_u16(row + nb - 1);
-                nb -= 1;
-            }
-        }
-        spares_update(nplus_ev ? ws.pos : 0u, w.z, w.w, sp0, sp1, nsp);
-        nm = nm + ((ch == 0u || (prolif && un == 1u)) ? 1u : 0u) - ((BD && ch == 2u) ? 1u : 0u);
-        n_un += (prolif && un != 0u) ? 1u : 0u;
-        n_pm += ch == 0u ? 1u : 0u;
-        n_pp += ch == 1u ? 1u : 0u;
-        n_dm += ch == 2u ? 1u : 0u;
-        n_dp += ch == 3u ? 1u : 0u;
-        e += 1;
-        if (f32t)
-            t32 = t32 + (float)tau;
-        else
-            t = t + tau;
-        if (hash_on) {
-            const uint64_t x = (uint64_t)ch | (prolif ? ((uint64_t)k1v << 2) : 0ull) |
-                               (nplus_ev ? ((uint64_t)idx << 20) : 0ull);
-            h = (h ^ x) * kFnvPrime;
         }
     }
 }
@@ -922,22 +923,25 @@ static const void* const kStepperTable[2][2][4] = {
 
 // bin-store variants: [birth_death][segregation][K = 64 | 256][u16 | u32 counters]; the 256-bin
 // u32 variant runs 64-lane blocks (its 72 KiB of LDS per 64 lanes)
-#define ECDNA_BIN_SEG(BD, SEG)                                                                             \
-    {{(const void*)ssa_stepper_bins<BD, SEG, 8, false, kStepperBlock>,                                      \
-      (const void*)ssa_stepper_bins<BD, SEG, 8, true, kStepperBlock>},                                      \
-     {(const void*)ssa_stepper_bins<BD, SEG, 32, false, kBinWideBlock>,                                     \
-      (const void*)ssa_stepper_bins<BD, SEG, 32, true, kBinWideBlock>}}
-#define ECDNA_BIN_TABLE(BD) \
-    {ECDNA_BIN_SEG(BD, 0), ECDNA_BIN_SEG(BD, 1), ECDNA_BIN_SEG(BD, 2), ECDNA_BIN_SEG(BD, 3)}
+#define ECDNA_BIN_SEG(BD, SEG, TF)                                                                         \
+    {{(const void*)ssa_stepper_bins<BD, SEG, 8, false, kStepperBlock, TF>,                                  \
+      (const void*)ssa_stepper_bins<BD, SEG, 8, true, kStepperBlock, TF>},                                  \
+     {(const void*)ssa_stepper_bins<BD, SEG, 32, false, kBinWideBlock, TF>,                                 \
+      (const void*)ssa_stepper_bins<BD, SEG, 32, true, kBinWideBlock, TF>}}
+#define ECDNA_BIN_TABLE(BD, TF) \
+    {ECDNA_BIN_SEG(BD, 0, TF), ECDNA_BIN_SEG(BD, 1, TF), ECDNA_BIN_SEG(BD, 2, TF), ECDNA_BIN_SEG(BD, 3, TF)}
 
-static const void* const kBinStepperTable[2][4][2][2] = {ECDNA_BIN_TABLE(false), ECDNA_BIN_TABLE(true)};
+// [TF: 0 = f64 time, no hash | 1 = runtime flags][birth_death][segregation][K 64 | 256][u16 | u32]
+static const void* const kBinStepperTable[2][2][4][2][2] = {{ECDNA_BIN_TABLE(false, 0), ECDNA_BIN_TABLE(true, 0)},
+                                                            {ECDNA_BIN_TABLE(false, 1), ECDNA_BIN_TABLE(true, 1)}};
 
 const void* stepper_kernel(int birth_death, int segregation, int window) {
     return kStepperTable[window ? 1 : 0][birth_death ? 1 : 0][segregation & 3];
 }
 
-const void* bin_stepper_kernel(int birth_death, int segregation, uint32_t bin_k, int c32) {
-    return kBinStepperTable[birth_death ? 1 : 0][segregation & 3][bin_k > 64 ? 1 : 0][c32 ? 1 : 0];
+const void* bin_stepper_kernel(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags) {
+    const int tf = (flags & (ECDNA_FLAG_TIME_F32 | ECDNA_FLAG_EVENT_HASH)) ? 1 : 0;
+    return kBinStepperTable[tf][birth_death ? 1 : 0][segregation & 3][bin_k > 64 ? 1 : 0][c32 ? 1 : 0];
 }
 
 int bin_stepper_block(uint32_t bin_k) { return bin_k > 64 ? kBinWideBlock : kStepperBlock; }
@@ -954,7 +958,7 @@ hipError_t launch_bin_stepper(const StepperArgs& a, int birth_death, int segrega
                               uint32_t blocks, hipStream_t stream) {
     StepperArgs copy = a;
     void* args[] = {&copy};
-    return hipLaunchKernel(bin_stepper_kernel(birth_death, segregation, bin_k, c32), dim3(blocks),
+    return hipLaunchKernel(bin_stepper_kernel(birth_death, segregation, bin_k, c32, a.flags), dim3(blocks),
                            dim3(bin_stepper_block(bin_k)), args, 0, stream);
 }
 

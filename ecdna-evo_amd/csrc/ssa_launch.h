@@ -75,8 +75,9 @@ const void* stepper_kernel(int birth_death, int segregation, int window);
 hipError_t launch_stepper(const StepperArgs& a, int birth_death, int segregation, int window, uint32_t blocks,
                           hipStream_t stream);
 // Bin store (ECDNA_FLAG_BIN_STORE): bin_k = 64 or 256 binned copy numbers; c32 = u32 counters
-// (cell_cap > 65535). bin_stepper_block = the variant's workgroup size.
-const void* bin_stepper_kernel(int birth_death, int segregation, uint32_t bin_k, int c32);
+// (cell_cap > 65535); flags selects the compile-time variant without f32 time and event hash when
+// neither is set. bin_stepper_block = the variant's workgroup size.
+const void* bin_stepper_kernel(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags);
 int bin_stepper_block(uint32_t bin_k);
 hipError_t launch_bin_stepper(const StepperArgs& a, int birth_death, int segregation, uint32_t bin_k, int c32,
                               uint32_t blocks, hipStream_t stream);

@@ -57,6 +57,19 @@ def test_gpu_bin_store_matches_oracle(name, engine_mod, oracle_mod):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(n for n, c in BIN_CASES.items() if not c.flags & 0x1))
+def test_gpu_bin_store_fast_variant_matches_oracle(name, engine_mod, oracle_mod):
+    """The bin store's compile-time variant for f64 time without the event hash (the bench's kernel):
+    every case with the hash switched off, all outputs but the (zero) hash bit for bit."""
+    import dataclasses
+
+    from ecdna_evo_amd import abi
+
+    spec = dataclasses.replace(BIN_CASES[name], flags=BIN_CASES[name].flags & ~abi.FLAG_EVENT_HASH, _keep=[])
+    _compare(engine_mod.run(spec, want_rows=True), oracle_mod.run(spec, mode="philox", want_rows=True), name)
+
+
+@pytest.mark.gpu
 def test_gpu_stop_reasons_and_errors_exercised(engine_mod):
     """The case list really reaches every stop reason and error code."""
     from ecdna_evo_amd import abi

@@ -1,6 +1,7 @@
 """Throughput of the engine on every BASELINE.json config shape that runs on one GPU
 (configs[1..4]; C4 and C5 as the per-GPU shard of their 8-GPU runs). Development/measurement tool.
-Usage: python tools/probe_configs.py [c2 c3 c4 c5]"""
+Usage: [PROBE_FLAGS=0x20] [PROBE_KMAX=256] python tools/probe_configs.py [c2 c3 c4 c5]"""
+import dataclasses
 import json
 import os
 import sys
@@ -44,6 +45,8 @@ CONFIGS = {
 def main():
     for name in sys.argv[1:] or list(CONFIGS):
         spec = CONFIGS[name]()
+        spec = dataclasses.replace(spec, flags=spec.flags | int(os.environ.get("PROBE_FLAGS", "0"), 0),
+                                   bin_kmax=int(os.environ.get("PROBE_KMAX", "0")), _keep=[])
         t0 = time.time()
         ctx = engine.Context(spec)
         reps = 1 if name == "c5" else 2
@@ -55,7 +58,7 @@ def main():
         res = ctx.download()
         t = res.totals
         ev = int(t["events"].sum())
-        print(json.dumps({"config": name, "replicates": spec.n_replicates, "events": ev, "stepper_ms": s_ms,
+        print(json.dumps({"config": name, "flags": spec.flags, "bin_kmax": spec.bin_kmax, "replicates": spec.n_replicates, "events": ev, "stepper_ms": s_ms,
                           "hist_ms": h_ms, "wall_ms": wall * 1e3, "events_per_s_kernel": ev / (s_ms * 1e-3),
                           "events_per_s_wall": ev / wall, "geometry": ctx.geometry(),
                           "stops": t["stop_reasons"].sum(axis=0).tolist(), "errors": int(t["errors"].sum()),
