@@ -52,6 +52,25 @@ B_SUMMARY = 88
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2
 
 
+def valu_measured_ceilings():
+    """Measured issue rates (wave-instr/s, whole chip) of single-opcode streams at full occupancy
+    (tools/valu_probe.hip -> profiles/r01g_valu_issue_probe.txt): the 2-cycle class (VOP2 and/or/xor/
+    add/sub/lshrrev/mov with VGPR operands, f32 add/mul) and the 4-cycle class (VOP3 encodings, SGPR
+    operands, lshlrev, bfe, 24/32-bit multiplies, conversions, f64 add/mul)."""
+    rates = {}
+    try:
+        with open(os.path.join(REPO, "profiles", "r01g_valu_issue_probe.txt")) as f:
+            for line in f:
+                parts = line.split()
+                if len(parts) >= 2 and parts[-1] == "chip":
+                    rates[parts[0]] = float(parts[-3])
+    except Exception:
+        pass
+    two = [rates[k] for k in ("and_b32", "xor_v", "add_u32_v", "mov_b32") if k in rates]
+    four = [rates[k] for k in ("add_u32", "lshl_add_u32", "bfe_u32", "add_f64", "mul_f64", "cvt_f64_u32") if k in rates]
+    return (sum(two) / len(two) if two else None, sum(four) / len(four) if four else None)
+
+
 def workload_spec(first: int, n: int, total: int, seed: int = 42, device: int = 0, store: str = "bins") -> abi.RunSpec:
     return abi.RunSpec(process=abi.BIRTH_DEATH, segregation=abi.SEG_BINOMIAL, rates=((1.0, 1.5, 0.3, 0.3),),
                        reps_per_set=total, seed=seed, first_replicate=first, n_replicates=n, max_cells=10_000,
@@ -213,14 +232,20 @@ def main():
         issue = None
         if args.store == "bins" and "valu_insts_per_event" in pmc:
             per_event = pmc["valu_insts_per_event"]
+            two, four = valu_measured_ceilings()
             issue = {
                 "valu_wave_insts_per_event": per_event,
                 "per_s": per_event * kernel_eps,
                 "peak_per_s": VALU_ISSUE_PEAK,
                 "frac": per_event * kernel_eps / VALU_ISSUE_PEAK,
+                "measured_2cycle_class_per_s": two,
+                "measured_4cycle_class_per_s": four,
+                "frac_of_measured_4cycle_class": per_event * kernel_eps / four if four else None,
                 "note": "the bin store keeps every common-case event in LDS and registers, so the stepper is "
-                        "bounded by vector-instruction issue, not HBM (DESIGN.md §5); wave64 VALU instructions "
-                        "per event (= per lane-event / 64) from the committed PMC summary (SQ_INSTS_VALU)",
+                        "bounded by vector-instruction issue, not HBM (DESIGN.md §5); VALU wave-instructions per "
+                        "event from the committed PMC summary (SQ_INSTS_VALU); the spec peak assumes 2 cycles per "
+                        "wave64 instruction, which only the VOP2 logic/add/mov class reaches on gfx950 — most of "
+                        "the stepper's instructions are in the measured 4-cycle class (tools/valu_probe.hip)",
             }
         if args.store == "rows" and "read_requests_per_event" in pmc:
             per_event = pmc["read_requests_per_event"] + pmc["write_requests_per_event"]
