@@ -71,10 +71,17 @@ def valu_measured_ceilings():
     return (sum(two) / len(two) if two else None, sum(four) / len(four) if four else None)
 
 
-def workload_spec(first: int, n: int, total: int, seed: int = 42, device: int = 0, store: str = "bins") -> abi.RunSpec:
+# bin store tunable: copy numbers 1..32 as LDS counters (4 groups: a shorter pick scan; at C3 a
+# picked cell has k > 32 with probability 0.6 %, those go to the large-k row). C3: 125 ms vs 132 ms with 64.
+BENCH_BIN_KMAX = 32
+
+
+def workload_spec(first: int, n: int, total: int, seed: int = 42, device: int = 0, store: str = "bins",
+                  bin_kmax: int = BENCH_BIN_KMAX) -> abi.RunSpec:
     return abi.RunSpec(process=abi.BIRTH_DEATH, segregation=abi.SEG_BINOMIAL, rates=((1.0, 1.5, 0.3, 0.3),),
                        reps_per_set=total, seed=seed, first_replicate=first, n_replicates=n, max_cells=10_000,
-                       hist_bins=1025, flags=abi.FLAG_BIN_STORE if store == "bins" else 0, device=device)
+                       hist_bins=1025, flags=abi.FLAG_BIN_STORE if store == "bins" else 0,
+                       bin_kmax=bin_kmax if store == "bins" else 0, device=device)
 
 
 def algorithmic_bytes(words, n_reps: int, init_cells: int = 1) -> int:
@@ -153,6 +160,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--reps-per-gpu", type=int, default=REPS_PER_GPU)
     ap.add_argument("--store", choices=("bins", "rows"), default="bins")
+    ap.add_argument("--bin-kmax", type=int, choices=(32, 64, 256), default=BENCH_BIN_KMAX)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -170,7 +178,8 @@ def main():
     total = reps * n_gpus
 
     first, n = shard.weak_range(rank, reps)
-    spec = workload_spec(first, n, total, device=local if distributed else 0, store=args.store)
+    spec = workload_spec(first, n, total, device=local if distributed else 0, store=args.store,
+                         bin_kmax=args.bin_kmax)
     ctx = engine.Context(spec)
     hist = torch.zeros(spec.hist_bins, dtype=torch.int64, device="cuda")
     tot = torch.zeros(16, dtype=torch.int64, device="cuda")
@@ -281,8 +290,8 @@ def main():
             "config": {
                 "workload": "C3 (BASELINE.json configs[2]): 2^20 replicates/GPU, birth-death b0=1 b1=1.5 "
                             "d0=d1=0.3, binomial segregation, init {1:1}, stop 1e4 cells or t=17, seed 42",
-                "cell_store": "bins (copy-number counters in LDS, k<=64; ECDNA_FLAG_BIN_STORE)" if args.store == "bins"
-                              else "rows (u16 per cell in HBM, swap_remove order)",
+                "cell_store": f"bins (copy-number counters in LDS, k<={args.bin_kmax}; ECDNA_FLAG_BIN_STORE)"
+                              if args.store == "bins" else "rows (u16 per cell in HBM, swap_remove order)",
                 "replicates_per_gpu": reps,
                 "replicates_total": total,
                 "events_per_step": events_per_step,

@@ -74,8 +74,9 @@ int validate(const ecdna_ssa_params_t* p) {
     if (p->n_replicates && (p->first_replicate + p->n_replicates - 1) / p->reps_per_set >= p->n_param_sets)
         return fail(ECDNA_E_INVALID, "replicate ids map past the last parameter set");
     if (p->cell_cap == 0) return fail(ECDNA_E_INVALID, "cell_cap must be >= 1");
-    if ((p->flags & ECDNA_FLAG_BIN_STORE) && p->bin_kmax != 0 && p->bin_kmax != 64 && p->bin_kmax != 256)
-        return fail(ECDNA_E_INVALID, "bin_kmax must be 0 (= 64), 64 or 256");
+    if ((p->flags & ECDNA_FLAG_BIN_STORE) && p->bin_kmax != 0 && p->bin_kmax != 32 && p->bin_kmax != 64 &&
+        p->bin_kmax != 256)
+        return fail(ECDNA_E_INVALID, "bin_kmax must be 0 (= 64), 32, 64 or 256");
     if (p->n_snapshots > ecdna::kMaxSnapshots) return fail(ECDNA_E_INVALID, "at most 64 snapshots");
     if (p->n_snapshots && !p->snapshot_cells) return fail(ECDNA_E_INVALID, "snapshot_cells is NULL");
     for (uint32_t q = 1; q < p->n_snapshots; ++q)

@@ -42,6 +42,34 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1
     return c;
 }
 
+// Philox4x32-10 with the 20 round keys precomputed per lane in VGPRs (philox_round_keys): no key
+// schedule on the SALU and no SALU-write -> VALU-read hazard waits inside the rounds. Same function.
+struct PhiloxKeys {
+    uint32_t k0[10], k1[10];
+};
+
+__device__ __forceinline__ PhiloxKeys philox_round_keys(uint32_t k0, uint32_t k1) {
+    PhiloxKeys r;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        uint32_t a = k0 + (uint32_t)i * kPhiloxW0, b = k1 + (uint32_t)i * kPhiloxW1;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(r.k0[i]) : "s"(a));  // pin to VGPRs
+        asm volatile("v_mov_b32 %0, %1" : "=v"(r.k1[i]) : "s"(b));
+    }
+    return r;
+}
+
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, const PhiloxKeys& rk) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)kPhiloxM0 * c.x;
+        const uint64_t p1 = (uint64_t)kPhiloxM1 * c.z;
+        c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ rk.k0[r], (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ rk.k1[r],
+                       (uint32_t)p0);
+    }
+    return c;
+}
+
 // -ln((w + 0.5) 2^-32), draw mapping v2: d = w + 0.5 = m 2^ex with m in [0.5, 1); the
 // top 7 fraction bits j of m pick {C, LN} = {1/mid_j, ln mid_j} (ssa_logtab.h, staged in LDS), r =
 // m C - 1 (|r| <= 2^-8, the subtraction exact), ln(1 + r) by a degree-7 series in explicit fmas, and

@@ -924,15 +924,17 @@ static const void* const kStepperTable[2][2][4] = {
 // bin-store variants: [birth_death][segregation][K = 64 | 256][u16 | u32 counters]; the 256-bin
 // u32 variant runs 64-lane blocks (its 72 KiB of LDS per 64 lanes)
 #define ECDNA_BIN_SEG(BD, SEG, TF)                                                                         \
-    {{(const void*)ssa_stepper_bins<BD, SEG, 8, false, kStepperBlock, TF>,                                  \
+    {{(const void*)ssa_stepper_bins<BD, SEG, 4, false, kStepperBlock, TF>,                                  \
+      (const void*)ssa_stepper_bins<BD, SEG, 4, true, kStepperBlock, TF>},                                  \
+     {(const void*)ssa_stepper_bins<BD, SEG, 8, false, kStepperBlock, TF>,                                  \
       (const void*)ssa_stepper_bins<BD, SEG, 8, true, kStepperBlock, TF>},                                  \
      {(const void*)ssa_stepper_bins<BD, SEG, 32, false, kBinWideBlock, TF>,                                 \
       (const void*)ssa_stepper_bins<BD, SEG, 32, true, kBinWideBlock, TF>}}
 #define ECDNA_BIN_TABLE(BD, TF) \
     {ECDNA_BIN_SEG(BD, 0, TF), ECDNA_BIN_SEG(BD, 1, TF), ECDNA_BIN_SEG(BD, 2, TF), ECDNA_BIN_SEG(BD, 3, TF)}
 
-// [TF: 0 = f64 time, no hash | 1 = runtime flags][birth_death][segregation][K 64 | 256][u16 | u32]
-static const void* const kBinStepperTable[2][2][4][2][2] = {{ECDNA_BIN_TABLE(false, 0), ECDNA_BIN_TABLE(true, 0)},
+// [TF: 0 = f64 time, no hash | 1 = runtime flags][birth_death][segregation][K 32 | 64 | 256][u16 | u32]
+static const void* const kBinStepperTable[2][2][4][3][2] = {{ECDNA_BIN_TABLE(false, 0), ECDNA_BIN_TABLE(true, 0)},
                                                             {ECDNA_BIN_TABLE(false, 1), ECDNA_BIN_TABLE(true, 1)}};
 
 const void* stepper_kernel(int birth_death, int segregation, int window) {
@@ -941,7 +943,8 @@ const void* stepper_kernel(int birth_death, int segregation, int window) {
 
 const void* bin_stepper_kernel(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags) {
     const int tf = (flags & (ECDNA_FLAG_TIME_F32 | ECDNA_FLAG_EVENT_HASH)) ? 1 : 0;
-    return kBinStepperTable[tf][birth_death ? 1 : 0][segregation & 3][bin_k > 64 ? 1 : 0][c32 ? 1 : 0];
+    return kBinStepperTable[tf][birth_death ? 1 : 0][segregation & 3][bin_k > 64 ? 2 : (bin_k > 32 ? 1 : 0)]
+                           [c32 ? 1 : 0];
 }
 
 int bin_stepper_block(uint32_t bin_k) { return bin_k > 64 ? kBinWideBlock : kStepperBlock; }

@@ -146,8 +146,8 @@ typedef struct {
      * into init_copies, init_set_nminus[n_param_sets]). Copy numbers must be >= 1. */
     const uint16_t* init_copies;    /* host */
     uint32_t init_nplus;
-    uint32_t bin_kmax;              /* ECDNA_FLAG_BIN_STORE: copy numbers 1..bin_kmax are binned; 64 or 256
-                                       (0 = 64); part of the draw mapping (the canonical cell order) */
+    uint32_t bin_kmax;              /* ECDNA_FLAG_BIN_STORE: copy numbers 1..bin_kmax are binned; 32, 64 or
+                                       256 (0 = 64); part of the draw mapping (the canonical cell order) */
     uint64_t init_nminus;
     const uint32_t* init_set_offsets; /* host or NULL */
     const uint64_t* init_set_nminus;  /* host or NULL */

@@ -697,7 +697,8 @@ static int validate(const ecdna_ssa_params_t* p, uint64_t row_stride, int want_r
         if (!p->init_set_offsets) break;
     }
     if (maxn > p->cell_cap) return ECDNA_E_INVALID;
-    if ((p->flags & ECDNA_FLAG_BIN_STORE) && p->bin_kmax != 0 && p->bin_kmax != 64 && p->bin_kmax != 256)
+    if ((p->flags & ECDNA_FLAG_BIN_STORE) && p->bin_kmax != 0 && p->bin_kmax != 32 && p->bin_kmax != 64 &&
+        p->bin_kmax != 256)
         return ECDNA_E_INVALID;
     if (want_rows && row_stride < p->cell_cap) return ECDNA_E_INVALID;
     if (p->n_snapshots > 64 || (p->n_snapshots && !p->snapshot_cells)) return ECDNA_E_INVALID;

@@ -101,6 +101,9 @@ def bin_cases():
     for name in ("bd_turnover", "big_copies", "abc_sets", "bd_snapshots", "pb_binomial_c1"):
         spec = cases()[name]
         c[f"bins256_{name}"] = dataclasses.replace(spec, flags=spec.flags | B, bin_kmax=256, _keep=[])
+    for name in ("bd_binomial", "bd_selection", "spares_mid_copies", "bd_snapshots", "abc_sets", "big_copies"):
+        spec = cases()[name]
+        c[f"bins32_{name}"] = dataclasses.replace(spec, flags=spec.flags | B, bin_kmax=32, _keep=[])
     c["bins_boundary_pb"] = abi.RunSpec(seed=41, n_replicates=32, max_cells=400, init={30: 2, 33: 1, 64: 2, 65: 2, 130: 1},
                                         hist_bins=300, flags=H | B)
     c["bins_boundary_bd"] = abi.RunSpec(seed=43, process=abi.BIRTH_DEATH, rates=((1.0, 1.3, 0.6, 0.7),),

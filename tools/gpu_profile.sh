@@ -5,6 +5,7 @@
 set -euo pipefail
 TAG=${1:-r01}
 STORE=${2:-bins}
+# (bench.py defaults: bin store with bin_kmax 32 for C3)
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/prof_$TAG
 mkdir -p $O
