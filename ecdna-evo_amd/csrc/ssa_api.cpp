@@ -569,12 +569,14 @@ int ecdna_ssa_ctx_download(ecdna_ssa_ctx* c, ecdna_rep_summary_t* out_summaries,
                 uint16_t* r = out_rows + i * c->row_stride;
                 uint64_t small = 0;
                 for (uint64_t b = 0; b < kb; ++b) small += bags[i * kb + b];
-                const uint64_t nbig = summ[i].nplus >= small ? summ[i].nplus - small : 0;
+                const uint64_t nbig = std::min<uint64_t>(summ[i].nplus >= small ? summ[i].nplus - small : 0,
+                                                         c->row_stride);
                 big.assign(r, r + nbig);
                 uint64_t pos = 0;
                 for (uint64_t b = 0; b < kb; ++b)
-                    for (uint32_t q = 0; q < bags[i * kb + b]; ++q) r[pos++] = (uint16_t)(b + 1);
-                std::copy(big.begin(), big.end(), r + pos);
+                    for (uint32_t q = 0; q < bags[i * kb + b] && pos < c->row_stride; ++q) r[pos++] = (uint16_t)(b + 1);
+                const uint64_t tail = std::min<uint64_t>(big.size(), c->row_stride - pos);
+                std::copy(big.begin(), big.begin() + tail, r + pos);
             }
         }
     }
