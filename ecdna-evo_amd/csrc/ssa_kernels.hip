@@ -389,8 +389,9 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
 // reads per lane; updates are fire-and-forget LDS atomic adds on the packed counters. In the common case
 // (every copy number involved <= K) an event touches no HBM at all.
 //
-// LDS per lane: counts NG*8 (u16, or u32 when C32) + NG group sums of the same width, laid out
-// [vector][lane] in 16-B vectors so a wave's 16-B reads are contiguous (conflict-free).
+// LDS per lane: counts NG*8 (u16, or u32 when C32) + NG group sums of the same width. u16 counters are
+// laid out [vector][lane] in 16-B vectors so a wave's 16-B reads are contiguous (conflict-free); u32
+// counters [counter][lane] (planar), see word_index.
 template <int NG, bool C32>
 struct BinLayout {
     static constexpr int kK = 8 * NG;                       // binned copy numbers 1..kK
@@ -426,11 +427,14 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
     // 32-bit word index (u32 math: LDS addresses stay 32-bit) of bin b / group g in the [vector][lane]
     // layout: vector b / kPerVec, word (b % kPerVec) / (counters per word). Indices are masked to their
     // range (b < K, g < NG) so the vector term folds away where it is constant.
+    // u32 counters (C32) use the planar layout instead: counter b of a lane at word b * BLK + lane, so
+    // an update is one shifted add off a per-lane base and the wave's 4-B atomics hit 64 consecutive
+    // words (no bank conflicts); the scans read single words at immediate offsets.
     uint32_t* const cnt_w = reinterpret_cast<uint32_t*>(&cnt_v[0][0]);
     uint32_t* const sum_w = reinterpret_cast<uint32_t*>(&sum_v[0][0]);
     const uint32_t lane4 = tid * 4u;
     auto word_index = [&](uint32_t b) -> uint32_t {
-        return C32 ? (b >> 2) * (BLK * 4u) + lane4 + (b & 3u) : (b >> 3) * (BLK * 4u) + lane4 + ((b >> 1) & 3u);
+        return C32 ? b * (uint32_t)BLK + tid : (b >> 3) * (BLK * 4u) + lane4 + ((b >> 1) & 3u);
     };
     auto bin_word = [&](uint32_t b) -> uint32_t* { return cnt_w + word_index(b); };
     auto shifted = [&](uint32_t idx, uint32_t d) -> uint32_t { return C32 ? d : (d << ((idx & 1u) * 16)); };
@@ -448,6 +452,23 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
     // every valid i). The same for the 8 bins of the group. Counts stay below 2^31.
     auto bin_find = [&](uint32_t i) -> uint32_t {
         uint32_t d = i, r = i, neg = 0;
+        if (C32) {
+#pragma unroll
+            for (int j = 0; j < NG - 1; ++j) {  // the last group closes the scan
+                d -= sum_w[j * BLK + tid];
+                neg += d >> 31;
+                r = min(r, d);
+            }
+            const uint32_t g = (uint32_t)(NG - 1) - neg;
+            const uint32_t* grp = cnt_w + g * (8u * BLK) + tid;
+            uint32_t d2 = r, neg2 = 0;
+#pragma unroll
+            for (int j = 0; j < 7; ++j) {
+                d2 -= grp[j * BLK];
+                neg2 += d2 >> 31;
+            }
+            return g * 8u + (7u - neg2) + 1u;
+        }
 #pragma unroll
         for (int v = 0; v < L::kSumVecs; ++v) {
             const uint4 sv = sum_v[v][tid];
@@ -474,6 +495,13 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
         return g * 8u + (7u - neg2) + 1u;
     };
     auto bins_zero = [&]() {
+        if (C32) {
+#pragma unroll 8
+            for (uint32_t b = 0; b < K; ++b) cnt_w[b * BLK + tid] = 0u;
+#pragma unroll
+            for (uint32_t g = 0; g < (uint32_t)NG; ++g) sum_w[g * BLK + tid] = 0u;
+            return;
+        }
 #pragma unroll
         for (int v = 0; v < L::kBinVecs; ++v) cnt_v[v][tid] = make_uint4(0, 0, 0, 0);
 #pragma unroll
@@ -515,8 +543,16 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             if (have) {
                 // final bin counters -> bags[li] (B stays in the row)
                 uint4* bag = reinterpret_cast<uint4*>(a.bags) + (uint64_t)li * L::kBinVecs;
+                if (C32) {
+#pragma unroll 8
+                    for (uint32_t v = 0; v < (uint32_t)L::kBinVecs; ++v) {
+                        const uint32_t* c = cnt_w + 4u * v * BLK + tid;
+                        bag[v] = make_uint4(c[0], c[BLK], c[2 * BLK], c[3 * BLK]);
+                    }
+                } else {
 #pragma unroll
-                for (int v = 0; v < L::kBinVecs; ++v) bag[v] = cnt_v[v][tid];
+                    for (int v = 0; v < L::kBinVecs; ++v) bag[v] = cnt_v[v][tid];
+                }
                 ecdna_rep_summary_t* s = a.summaries + li;
                 s->nminus = nm;
                 s->nplus = ns + nb;
