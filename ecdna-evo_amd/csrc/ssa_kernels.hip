@@ -106,7 +106,11 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
     float b0 = 0.f, b1 = 0.f, d0 = 0.f, d1 = 0.f;
     double t = 0.0;
     float t32 = 0.f;
-    uint32_t e = 0, n_pm = 0, n_pp = 0, n_dm = 0, n_dp = 0, n_un = 0;
+    // Per-type event counts: only DeathNMinus (BD) and uneven splits are counted per event; the other
+    // three follow at the end from the event total and the population changes (src/proliferation.rs:
+    // an even split adds one N+ cell, an uneven one none (plus an N- cell unless NoNminus), a death
+    // removes one): dnp = pp - un - dp, dnm = pm - dm + un(with an N- daughter), e = pm + pp + dm + dp.
+    uint32_t e = 0, n_dm = 0, n_un = 0, np0 = 0, nm0 = 0;
     uint64_t h = kFnvOffset;
     uint32_t stop = 0, err = 0;
     uint32_t sj = 0;  // snapshots popped so far (the deque's front index)
@@ -120,11 +124,18 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
                 s->nminus = nm;
                 s->nplus = np;
                 s->iters = e;
-                s->events_by_type[0] = n_pm;
-                s->events_by_type[1] = n_pp;
-                s->events_by_type[2] = n_dm;
-                s->events_by_type[3] = n_dp;
-                s->uneven = n_un;
+                {
+                    const uint32_t un1 = SEG == ECDNA_SEG_BINOMIAL_NO_NMINUS ? 0u : n_un;  // uneven with an N- daughter
+                    const uint32_t n_pm = nm - nm0 + n_dm - un1;                          // (mod 2^32)
+                    const uint32_t pp_minus_dp = np - np0 + n_un;
+                    const uint32_t pp_plus_dp = e - n_pm - n_dm;
+                    const uint32_t n_pp = (pp_plus_dp + pp_minus_dp) >> 1;
+                    s->events_by_type[0] = n_pm;
+                    s->events_by_type[1] = n_pp;
+                    s->events_by_type[2] = n_dm;
+                    s->events_by_type[3] = pp_plus_dp - n_pp;
+                    s->uneven = n_un;
+                }
                 s->time = f32t ? (double)t32 : t;
                 s->event_hash = hash_on ? h : 0ull;
                 s->stop_reason = stop;
@@ -162,7 +173,9 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
             if (WIN && cnt) tail = src[cnt - 1];
             t = 0.0;
             t32 = 0.f;
-            e = n_pm = n_pp = n_dm = n_dp = n_un = 0;
+            e = n_dm = n_un = 0;
+            np0 = np;
+            nm0 = nm;
             nsp = 0;
             h = kFnvOffset;
             stop = 0;
@@ -367,10 +380,7 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
         spares_update((ch & 1u) ? ws.pos : 0u, w.z, w.w, sp0, sp1, nsp);
         // increase_nminus / decrease_nminus (src/proliferation.rs:113-117, 135-139) and the counters
         nm = nm + (ch == 0u ? 1u : 0u) - (ch == 2u ? 1u : 0u);
-        n_pm += ch == 0u ? 1u : 0u;
-        n_pp += ch == 1u ? 1u : 0u;
-        n_dm += ch == 2u ? 1u : 0u;
-        n_dp += ch == 3u ? 1u : 0u;
+        if (BD) n_dm += ch == 2u ? 1u : 0u;
         e += 1;
         if (f32t)
             t32 = t32 + (float)tau;
@@ -533,7 +543,11 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
     double rb0 = 0.0, rb1 = 0.0, rd0 = 0.0, rd1 = 0.0;  // the f32 rates, widened once per replicate
     double t = 0.0;
     float t32 = 0.f;
-    uint32_t e = 0, n_pm = 0, n_pp = 0, n_dm = 0, n_dp = 0, n_un = 0;
+    // Per-type event counts: only DeathNMinus (BD) and uneven splits are counted per event; the other
+    // three follow at the end from the event total and the population changes (src/proliferation.rs:
+    // an even split adds one N+ cell, an uneven one none (plus an N- cell unless NoNminus), a death
+    // removes one): dnp = pp - un - dp, dnm = pm - dm + un(with an N- daughter), e = pm + pp + dm + dp.
+    uint32_t e = 0, n_dm = 0, n_un = 0, np0 = 0, nm0 = 0;
     uint64_t h = kFnvOffset;
     uint32_t stop = 0, err = 0;
     uint32_t sj = 0;
@@ -557,11 +571,18 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                 s->nminus = nm;
                 s->nplus = ns + nb;
                 s->iters = e;
-                s->events_by_type[0] = n_pm;
-                s->events_by_type[1] = n_pp;
-                s->events_by_type[2] = n_dm;
-                s->events_by_type[3] = n_dp;
-                s->uneven = n_un;
+                {
+                    const uint32_t un1 = SEG == ECDNA_SEG_BINOMIAL_NO_NMINUS ? 0u : n_un;  // uneven with an N- daughter
+                    const uint32_t n_pm = nm - nm0 + n_dm - un1;                          // (mod 2^32)
+                    const uint32_t pp_minus_dp = (ns + nb) - np0 + n_un;
+                    const uint32_t pp_plus_dp = e - n_pm - n_dm;
+                    const uint32_t n_pp = (pp_plus_dp + pp_minus_dp) >> 1;
+                    s->events_by_type[0] = n_pm;
+                    s->events_by_type[1] = n_pp;
+                    s->events_by_type[2] = n_dm;
+                    s->events_by_type[3] = pp_plus_dp - n_pp;
+                    s->uneven = n_un;
+                }
                 s->time = f32t ? (double)t32 : t;
                 s->event_hash = hash_on ? h : 0ull;
                 s->stop_reason = stop;
@@ -602,7 +623,9 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             nm = (uint32_t)(a.init_nminus_set ? a.init_nminus_set[set] : a.init_nminus);
             t = 0.0;
             t32 = 0.f;
-            e = n_pm = n_pp = n_dm = n_dp = n_un = 0;
+            e = n_dm = n_un = 0;
+            np0 = ns + nb;
+            nm0 = nm;
             nsp = 0;
             h = kFnvOffset;
             stop = 0;
@@ -747,9 +770,10 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                 const bool sa = has_a && da <= K, sb = has_b && db <= K;
                 const uint32_t ns_old = ns;
                 // common case: every copy number involved is binned -> LDS only, no branch
-                bin_add(small ? k : 1u, (nplus_ev && small) ? 0xffffffffu : 0u);
-                bin_add(sa ? da : 1u, sa ? 1u : 0u);
-                bin_add(sb ? db : 1u, sb ? 1u : 0u);
+                // (bin_add masks its copy number into range, so lanes adding 0 need no select)
+                bin_add(k, (nplus_ev && small) ? 0xffffffffu : 0u);
+                bin_add(da, sa ? 1u : 0u);
+                bin_add(db, sb ? 1u : 0u);
                 ns = ns - ((nplus_ev && small) ? 1u : 0u) + (sa ? 1u : 0u) + (sb ? 1u : 0u);
                 if (nplus_ev && (!small || (has_a && !sa) || (has_b && !sb))) {  // the large-k row (rare)
                     uint32_t open = small ? 0xffffffffu : idx - ns_old;  // B slot freed by a large picked cell
@@ -777,10 +801,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                 spares_update(nplus_ev ? ws.pos : 0u, w.z, w.w, sp0, sp1, nsp);
                 nm = nm + ((ch == 0u || (prolif && un == 1u)) ? 1u : 0u) - ((BD && ch == 2u) ? 1u : 0u);
                 n_un += (prolif && un != 0u) ? 1u : 0u;
-                n_pm += ch == 0u ? 1u : 0u;
-                n_pp += ch == 1u ? 1u : 0u;
-                n_dm += ch == 2u ? 1u : 0u;
-                n_dp += ch == 3u ? 1u : 0u;
+                if (BD) n_dm += ch == 2u ? 1u : 0u;
                 e += 1;
                 if (f32t)
                     t32 = t32 + (float)tau;
