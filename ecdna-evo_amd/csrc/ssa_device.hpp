@@ -75,6 +75,14 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, const PhiloxKeys& rk) {
 // m C - 1 (|r| <= 2^-8, the subtraction exact), ln(1 + r) by a degree-7 series in explicit fmas, and
 // -ln u = -(LN + ln(1 + r) + (ex - 32) ln 2). oracle_softlog_neg (oracle/ssa_oracle.c) performs the
 // same IEEE operations in the same order, so CPU and GPU agree bit for bit.
+// v_fma_f64 in its 3-address (VOP3) form: left to itself the compiler picks the 2-address v_fmac_f64
+// plus a v_mov_b64 of the addend for each Horner step. Same correctly rounded fma.
+__device__ __forceinline__ double fma3(double a, double b, double c) {
+    double d;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
 __device__ __forceinline__ double softlog_neg(uint32_t w, const double2* tab) {
     const double d = (double)w + 0.5;  // exact
     const uint64_t bits = (uint64_t)__double_as_longlong(d);
@@ -83,11 +91,11 @@ __device__ __forceinline__ double softlog_neg(uint32_t w, const double2* tab) {
     const double m = __longlong_as_double((long long)((bits & 0x000fffffffffffffull) | (1022ull << 52)));
     const double2 cl = tab[(hi >> 13) & 127u];
     const double r = m * cl.x - 1.0;
-    double q = fma(r, 0x1.2492492492492p-3, -0x1.5555555555555p-3);  // 1/7, -1/6
-    q = fma(r, q, 0x1.999999999999ap-3);                                // 1/5
-    q = fma(r, q, -0x1p-2);                                             // -1/4
-    q = fma(r, q, 0x1.5555555555555p-2);                                // 1/3
-    q = fma(r, q, -0x1p-1);                                             // -1/2
+    double q = fma3(r, 0x1.2492492492492p-3, -0x1.5555555555555p-3);  // 1/7, -1/6
+    q = fma3(r, q, 0x1.999999999999ap-3);                                // 1/5
+    q = fma3(r, q, -0x1p-2);                                             // -1/4
+    q = fma3(r, q, 0x1.5555555555555p-2);                                // 1/3
+    q = fma3(r, q, -0x1p-1);                                             // -1/2
     const double l = fma(r * r, q, r);                                  // ln(1 + r)
     return -fma((double)(ex - 32), 0x1.62e42fefa39efp-1, cl.y + l);
 }

@@ -719,12 +719,12 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             uint32_t ev_err = 0;
             if (SEG != ECDNA_SEG_DETERMINISTIC) {
                 // popcount of the stream's next n bits: w3 alone (k <= 16) or w3 and the first spare (k <= 32)
-                const uint32_t nh = n - 32u;
                 const bool fast1 = ws.pos == 1 && n <= 32u;
                 const bool fast2 = ws.pos == 1 && n > 32u && n <= 64u && nsp >= 1u;
                 const bool fast = fast1 || fast2;
-                k1v = fast1 ? __popc(w.w & (n >= 32u ? 0xffffffffu : ((1u << (n & 31u)) - 1u)))
-                            : __popc(w.w) + __popc(sp0 & (nh >= 32u ? 0xffffffffu : ((1u << (nh & 31u)) - 1u)));
+                // branch-free: the low n bits of the 64-bit word (spare0 : w3), n clamped to 64
+                const uint64_t m64 = ~0ull >> (64u - min(n, 64u));
+                k1v = __popc(w.w & (uint32_t)m64) + __popc(sp0 & (uint32_t)(m64 >> 32));
                 if (prolif && fast) ws.pos = fast1 ? 2u : 3u;
                 if (prolif && !fast && k <= 32767u) {  // larger copy numbers or a rejected pick: more words
                     k1v = ws.binomial_half(n);
