@@ -83,6 +83,13 @@ __device__ __forceinline__ double fma3(double a, double b, double c) {
     return d;
 }
 
+// 32 x 32 -> 64-bit product as one v_mad_u64_u32 (the compiler widens a u32 * u64 into two)
+__device__ __forceinline__ uint64_t mul_u32_wide(uint32_t a, uint32_t b) {
+    uint64_t d, carry;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(d), "=s"(carry) : "v"(a), "v"(b));
+    return d;
+}
+
 __device__ __forceinline__ double softlog_neg(uint32_t w, const double2* tab) {
     const double d = (double)w + 0.5;  // exact
     const uint64_t bits = (uint64_t)__double_as_longlong(d);

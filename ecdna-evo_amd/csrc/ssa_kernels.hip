@@ -430,6 +430,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
     const uint32_t tid = threadIdx.x;
     const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
     const PhiloxKeys rk = philox_round_keys(k0, k1);  // event blocks: round keys in VGPRs
+    const uint32_t stop32 = a.stop_cells < 0xffffffffull ? (uint32_t)a.stop_cells : 0xffffffffu;
 
     // packed counter add: bin b (0-based, copy number b + 1) / group g, by +d (d = +1, -1 or 0, as a
     // two's complement 32-bit word: a 16-bit field never borrows from its neighbour because it is >= 1
@@ -651,7 +652,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
         }
         // stop checks: one test here, the reason only when a lane stops
         const bool t_over = f32t ? (t32 >= a.max_time32) : (t >= a.max_time);
-        const bool cells_over = (uint64_t)nm + np >= a.stop_cells;
+        const bool cells_over = nm + np >= stop32;  // (u32: cell counts stay below 2^32)
         if ((e >= a.max_iter) || cells_over || t_over || !(a0 > 0.0)) {
             stop = (e >= a.max_iter) ? (uint32_t)ECDNA_STOP_MAX_ITER
                    : cells_over     ? (uint32_t)ECDNA_STOP_MAX_CELLS
@@ -680,7 +681,8 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             const uint4 w = philox4x32_10(make_uint4(e, 0u, rid_lo, rid_hi), rk);
             // direct method: the channel is the number of cumulative propensities <= target (the first i
             // with target < c_i; the c_i are non-decreasing)
-            const double target = (((double)w.y + 0.5) * 0x1p-32) * a0;
+            // (w1 + 0.5) 2^-32 formed exactly by one fma (the same value the oracle's add and scaling give)
+            const double target = fma3((double)w.y, 0x1p-32, 0x1p-33) * a0;
             uint32_t ch = (target >= cA ? 1u : 0u);
             if (BD) ch += (target >= cB ? 1u : 0u) + (target >= cC ? 1u : 0u);
             const bool nplus_ev = (ch & 1u) != 0;  // ProliferateNPlus or DeathNPlus: a cell is picked
@@ -698,11 +700,10 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             ws.k0 = k0;
             ws.k1 = k1;
             ws.pos = 1;
-            ws.blk_id = 0;
-            ws.blk = make_uint4(0, 0, 0, 0);
+            ws.blk_id = 0;  // (ws.blk is only read after the block it holds was generated)
 
             // uniform N+ cell: Lemire multiply-shift on w2; exact rejection (rare) from the stream
-            uint64_t m = (uint64_t)w.z * np;
+            uint64_t m = mul_u32_wide(w.z, np);
             if (nplus_ev && (uint32_t)m < np) {
                 const uint32_t thr = (0u - np) % np;
                 while ((uint32_t)m < thr) m = (uint64_t)ws.next() * np;
