@@ -453,6 +453,18 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
         a.bags = c->d_bags;
         const uint32_t need = (ch.n + c->stepper_block - 1) / c->stepper_block;
         const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(need, c->stepper_blocks_cap));
+        // Drain control (bin store, 256-lane blocks, one wave per SIMD per block): when lanes run more than
+        // two replicates each, the youngest wave slot of every SIMD stops taking fresh replicates once
+        // fewer than 1.5 grids' worth are left (C3: 105 -> 101 ms). ECDNA_SSA_ADMIT=0: off.
+        a.admit_slot = 0xffffffffu;
+        a.admit_remaining = 0;
+        const uint64_t lanes = (uint64_t)blocks * c->stepper_block;
+        const uint32_t per_cu = c->cus ? (uint32_t)((blocks + c->cus - 1) / c->cus) : 0u;
+        if (c->bin_k && c->stepper_block == 256 && per_cu >= 2 && ch.n > 2 * lanes &&
+            env_u64("ECDNA_SSA_ADMIT", 1)) {
+            a.admit_slot = per_cu - 1;
+            a.admit_remaining = (uint32_t)std::min<uint64_t>(lanes + lanes / 2, ch.n);
+        }
 
         HIP_TRY(hipEventRecord(ch.ev[0], st));
         if (c->bin_k)

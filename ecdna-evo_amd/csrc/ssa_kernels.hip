@@ -535,6 +535,13 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
     const bool f32t = TF ? (a.flags & ECDNA_FLAG_TIME_F32) != 0 : false;
     const bool hash_on = TF ? (a.flags & ECDNA_FLAG_EVENT_HASH) != 0 : false;
 
+    // Drain control (speed only; results depend on replicate ids alone): a SIMD's arbiter favours its
+    // older waves, so a replicate started near the end on the youngest wave runs 2-3x
+    // longer than on the oldest. The youngest wave slot of each SIMD (HW_ID wave id == admit_slot)
+    // stops taking fresh replicates once fewer than admit_remaining are left.
+    unsigned hw_id;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_id));
+    const bool young = (hw_id & 15u) == a.admit_slot;
     bool active = false, have = false;
     uint32_t li = 0;
     uint64_t rid = 0;
@@ -589,6 +596,8 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                 s->stop_reason = stop;
                 s->error = err;
             }
+            if (young && __hip_atomic_load(a.head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + a.admit_remaining >= a.n)
+                break;
             const uint32_t i = atomicAdd(a.head, 1u);
             if (i >= a.n) break;
             have = true;
