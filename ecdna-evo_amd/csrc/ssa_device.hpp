@@ -59,13 +59,49 @@ __device__ __forceinline__ PhiloxKeys philox_round_keys(uint32_t k0, uint32_t k1
     return r;
 }
 
+// a ^ b ^ c as one gfx950 v_bitop3_b32 (truth table 0x96) instead of two v_xor_b32
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, const PhiloxKeys& rk) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         const uint64_t p0 = (uint64_t)kPhiloxM0 * c.x;
         const uint64_t p1 = (uint64_t)kPhiloxM1 * c.z;
-        c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ rk.k0[r], (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ rk.k1[r],
-                       (uint32_t)p0);
+        c = make_uint4(xor3((uint32_t)(p1 >> 32), c.y, rk.k0[r]), (uint32_t)p1,
+                       xor3((uint32_t)(p0 >> 32), c.w, rk.k1[r]), (uint32_t)p0);
+    }
+    return c;
+}
+
+// The bin store's event block is Philox((e, 0, rid_lo, rid_hi)): round 0's c.z product and the words
+// it is XORed with depend only on the replicate, so they are formed once per replicate.
+struct PhiloxEventPre {
+    uint32_t x0, x1, x2;  // round-0 outputs 0 and 1; rid_hi ^ k1[0] for output 2
+};
+
+__device__ __forceinline__ PhiloxEventPre philox_event_pre(uint32_t rid_lo, uint32_t rid_hi, const PhiloxKeys& rk) {
+    const uint64_t p1 = (uint64_t)kPhiloxM1 * rid_lo;
+    PhiloxEventPre p;
+    p.x0 = (uint32_t)(p1 >> 32) ^ rk.k0[0];  // (c.y = 0)
+    p.x1 = (uint32_t)p1;
+    p.x2 = rid_hi ^ rk.k1[0];
+    return p;
+}
+
+// == philox4x32_10(make_uint4(e, 0, rid_lo, rid_hi), rk) for the pre formed from (rid_lo, rid_hi)
+__device__ __forceinline__ uint4 philox_event(uint32_t e, const PhiloxEventPre& pre, const PhiloxKeys& rk) {
+    const uint64_t p0 = (uint64_t)kPhiloxM0 * e;
+    uint4 c = make_uint4(pre.x0, pre.x1, (uint32_t)(p0 >> 32) ^ pre.x2, (uint32_t)p0);
+#pragma unroll
+    for (int r = 1; r < 10; ++r) {
+        const uint64_t q0 = (uint64_t)kPhiloxM0 * c.x;
+        const uint64_t q1 = (uint64_t)kPhiloxM1 * c.z;
+        c = make_uint4(xor3((uint32_t)(q1 >> 32), c.y, rk.k0[r]), (uint32_t)q1,
+                       xor3((uint32_t)(q0 >> 32), c.w, rk.k1[r]), (uint32_t)q0);
     }
     return c;
 }

@@ -430,6 +430,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
     const uint32_t tid = threadIdx.x;
     const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
     const PhiloxKeys rk = philox_round_keys(k0, k1);  // event blocks: round keys in VGPRs
+    PhiloxEventPre pre{0u, 0u, 0u};  // the replicate-only part of round 0
     const uint32_t stop32 = a.stop_cells < 0xffffffffull ? (uint32_t)a.stop_cells : 0xffffffffu;
 
     // packed counter add: bin b (0-based, copy number b + 1) / group g, by +d (d = +1, -1 or 0, as a
@@ -604,6 +605,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             active = true;
             li = i;
             rid = a.rid0 + i;
+            pre = philox_event_pre((uint32_t)rid, (uint32_t)(rid >> 32), rk);
             row = a.rows + (uint64_t)i * a.row_stride;
             const uint64_t set = rid / a.reps_per_set;
             const float4 r = a.rates[set];
@@ -687,7 +689,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             }
 
             const uint32_t rid_lo = (uint32_t)rid, rid_hi = (uint32_t)(rid >> 32);
-            const uint4 w = philox4x32_10(make_uint4(e, 0u, rid_lo, rid_hi), rk);
+            const uint4 w = philox_event(e, pre, rk);
             // direct method: the channel is the number of cumulative propensities <= target (the first i
             // with target < c_i; the c_i are non-decreasing)
             // (w1 + 0.5) 2^-32 formed exactly by one fma (the same value the oracle's add and scaling give)
