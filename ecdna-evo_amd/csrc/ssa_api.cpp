@@ -463,7 +463,8 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
         if (c->bin_k && c->stepper_block == 256 && per_cu >= 2 && ch.n > 2 * lanes &&
             env_u64("ECDNA_SSA_ADMIT", 1)) {
             a.admit_slot = per_cu - 1;
-            a.admit_remaining = (uint32_t)std::min<uint64_t>(lanes + lanes / 2, ch.n);
+            const uint64_t x8 = env_u64("ECDNA_SSA_ADMIT_X8", 12);  // eighths of a grid (tuning)
+            a.admit_remaining = (uint32_t)std::min<uint64_t>(lanes * x8 / 8, ch.n);
         }
 
         HIP_TRY(hipEventRecord(ch.ev[0], st));
