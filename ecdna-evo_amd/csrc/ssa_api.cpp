@@ -462,7 +462,8 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
         const uint32_t per_cu = c->cus ? (uint32_t)((blocks + c->cus - 1) / c->cus) : 0u;
         if (c->bin_k && c->stepper_block == 256 && per_cu >= 2 && ch.n > 2 * lanes &&
             env_u64("ECDNA_SSA_ADMIT", 1)) {
-            a.admit_slot = per_cu - 1;
+            const uint32_t slots = (uint32_t)std::min<uint64_t>(env_u64("ECDNA_SSA_ADMIT_SLOTS", 1), per_cu - 1);
+            a.admit_slot = per_cu - std::max<uint32_t>(slots, 1u);
             const uint64_t x8 = env_u64("ECDNA_SSA_ADMIT_X8", 12);  // eighths of a grid (tuning)
             a.admit_remaining = (uint32_t)std::min<uint64_t>(lanes * x8 / 8, ch.n);
         }

@@ -538,11 +538,11 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
 
     // Drain control (speed only; results depend on replicate ids alone): a SIMD's arbiter favours its
     // older waves, so a replicate started near the end on the youngest wave runs 2-3x
-    // longer than on the oldest. The youngest wave slot of each SIMD (HW_ID wave id == admit_slot)
+    // longer than on the oldest. The youngest wave slot(s) of each SIMD (HW_ID wave id >= admit_slot)
     // stops taking fresh replicates once fewer than admit_remaining are left.
     unsigned hw_id;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_id));
-    const bool young = (hw_id & 15u) == a.admit_slot;
+    const bool young = (hw_id & 15u) >= a.admit_slot;  // (0xffffffff: off)
     bool active = false, have = false;
     uint32_t li = 0;
     uint64_t rid = 0;

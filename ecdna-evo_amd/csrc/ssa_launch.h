@@ -38,7 +38,7 @@ struct StepperArgs {
     ecdna_snapshot_t* snap_meta;    // [n][n_snap], chunk-offset
     uint16_t* snap_rows;            // [n][n_snap][row_stride] or nullptr, chunk-offset
     void* bags;                     // bin store: [n][bin_k] final u16 / u32 bin counters (chunk-local)
-    // bin store drain control: waves in SIMD wave slot admit_slot (the youngest) take no fresh
+    // bin store drain control: waves in SIMD wave slots >= admit_slot (the youngest) take no fresh
     // replicate once fewer than admit_remaining are left; admit_slot = 0xffffffff: off
     uint32_t admit_slot;
     uint32_t admit_remaining;
