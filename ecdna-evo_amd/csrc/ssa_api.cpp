@@ -99,6 +99,9 @@ struct Chunk {
     uint64_t first;  // local index of the first replicate
     uint32_t n;
     hipEvent_t ev[3];
+    // replicate rotation (bin store; 0 = off): partition size and the counters it starts from
+    uint32_t rot_n_pad = 0;
+    std::vector<ecdna::RotPart> rot_init;
 };
 
 }  // namespace
@@ -139,6 +142,12 @@ struct ecdna_ssa_ctx {
     uint16_t* d_rows = nullptr;
     ecdna_rep_summary_t* d_summ = nullptr;
     uint32_t* d_heads = nullptr;  // one work counter per chunk
+    // replicate rotation (bin store): per-partition counters, state bytes, parked scalars (one chunk's worth)
+    ecdna::RotPart* d_rot_parts = nullptr;
+    uint32_t* d_rot_flags = nullptr;
+    uint4* d_rot_park = nullptr;
+    uint32_t rot_tick_log2 = 11;
+    int32_t rot_park_min = 0;
     uint64_t* d_hist_own = nullptr;
     ecdna_totals_t* d_tot_own = nullptr;
     uint64_t* d_hist = nullptr;
@@ -187,6 +196,9 @@ void free_ctx(ecdna_ssa_ctx* c) {
     (void)hipFree(c->d_bags);
     (void)hipFree(c->d_summ);
     (void)hipFree(c->d_heads);
+    (void)hipFree(c->d_rot_parts);
+    (void)hipFree(c->d_rot_flags);
+    (void)hipFree(c->d_rot_park);
     (void)hipFree(c->d_hist_own);
     (void)hipFree(c->d_tot_own);
     delete c;
@@ -348,7 +360,8 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
     }
 
     // rows: one u16 row per replicate of the chunk; chunk bounded by free HBM
-    const uint64_t row_bytes = c->row_stride * sizeof(uint16_t) + bag_bytes;
+    const uint64_t rot_bytes = c->bin_k ? ecdna::kParkVecs * 16u + 4u : 0u;  // parked scalars + state word
+    const uint64_t row_bytes = c->row_stride * sizeof(uint16_t) + bag_bytes + rot_bytes;
     size_t free_b = 0, total_b = 0;
     CTX_TRY(hipMemGetInfo(&free_b, &total_b));
     uint64_t budget = (uint64_t)((double)free_b * 0.85);
@@ -394,6 +407,41 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
     c->stepper_blocks_cap = (uint32_t)(per_cu * c->cus);
     uint64_t max_blocks = env_u64("ECDNA_SSA_MAX_BLOCKS", 0);  // testing: force lane refill
     if (max_blocks) c->stepper_blocks_cap = (uint32_t)std::min<uint64_t>(c->stepper_blocks_cap, max_blocks);
+
+    // Replicate rotation (bin store, 256-lane blocks): on when a lane has at least two
+    // replicates to run (ECDNA_SSA_ROTATE = 0 off, 1 on whenever possible, 2 auto). Results do not depend
+    // on it. Byte offsets into bags/park are u32 in the kernel: chunks stay below 2 GiB of either.
+    const uint64_t rot_mode = env_u64("ECDNA_SSA_ROTATE", 2);
+    c->rot_tick_log2 = (uint32_t)std::min<uint64_t>(env_u64("ECDNA_SSA_ROT_TICK", 10), 30);
+    bool any_rot = false;
+    for (auto& ch : c->chunks) {
+        const uint64_t need = (ch.n + c->stepper_block - 1) / c->stepper_block;
+        const uint64_t lanes = std::max<uint64_t>(1, std::min<uint64_t>(need, c->stepper_blocks_cap)) * c->stepper_block;
+        const bool ok = c->bin_k && c->stepper_block == ecdna::kStepperBlock &&
+                        (uint64_t)ch.n * std::max<uint64_t>(bag_bytes, ecdna::kParkVecs * 16u) < (1ull << 31);
+        if (!ok || rot_mode == 0 || (rot_mode == 2 && ch.n < 2 * lanes)) continue;
+        const uint32_t per = (ch.n + ecdna::kRotParts - 1) / ecdna::kRotParts;
+        ch.rot_n_pad = (per + ecdna::kRotBlock - 1) / ecdna::kRotBlock * ecdna::kRotBlock;
+        ch.rot_init.assign(ecdna::kRotParts, ecdna::RotPart{});
+        for (uint32_t x = 0; x < ecdna::kRotParts; ++x) {
+            const uint64_t lo = (uint64_t)x * ch.rot_n_pad, hi = std::min<uint64_t>(lo + ch.rot_n_pad, ch.n);
+            const int cnt = hi > lo ? (int)(hi - lo) : 0;
+            ch.rot_init[x].waiting = cnt;
+            ch.rot_init[x].fresh = cnt;
+        }
+        any_rot = true;
+    }
+    if (any_rot) {
+        const uint64_t n_pad_max = (c->chunk_reps + ecdna::kRotParts - 1) / ecdna::kRotParts + ecdna::kRotBlock;
+        CTX_TRY(hipMalloc(&c->d_rot_parts, ecdna::kRotParts * sizeof(ecdna::RotPart)));
+        CTX_TRY(hipMalloc(&c->d_rot_flags, ecdna::kRotParts * n_pad_max * sizeof(uint32_t)));
+        CTX_TRY(hipMalloc(&c->d_rot_park, c->chunk_reps * ecdna::kParkVecs * sizeof(uint4)));
+        // park only while at least 1.5 partition grids' worth of replicates wait; below that the lanes run
+        // their replicates to the end (C3 sweep, DESIGN.md §5: 0.5 / 1 / 2 / 3 grids -> 88.2 / 87.2 / 87.1 / 97.5 ms)
+        const uint64_t lanes_all = (uint64_t)c->stepper_blocks_cap * c->stepper_block;
+        c->rot_park_min = (int32_t)env_u64("ECDNA_SSA_ROT_PARK_MIN",
+                                           std::max<uint64_t>(1, lanes_all * 3 / 2 / ecdna::kRotParts));
+    }
     *out = c;
     return ECDNA_OK;
 #undef CTX_TRY
@@ -466,6 +514,21 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
             a.admit_slot = per_cu - std::max<uint32_t>(slots, 1u);
             const uint64_t x8 = env_u64("ECDNA_SSA_ADMIT_X8", 12);  // eighths of a grid (tuning)
             a.admit_remaining = (uint32_t)std::min<uint64_t>(lanes * x8 / 8, ch.n);
+        }
+        if (ch.rot_n_pad) {  // rotation replaces the drain control
+            a.admit_slot = 0xffffffffu;
+            a.rot_parts = c->d_rot_parts;
+            a.rot_flags = c->d_rot_flags;
+            a.rot_park = c->d_rot_park;
+            a.rot_n_pad = ch.rot_n_pad;
+            a.rot_tick_log2 = c->rot_tick_log2;
+            a.rot_park_min = c->rot_park_min;
+            const uint64_t n_flags = (uint64_t)ecdna::kRotParts * ch.rot_n_pad;
+            HIP_TRY(hipMemsetD32Async(c->d_rot_flags, ecdna::ROT_FRESH, ch.n, st));
+            if (n_flags > ch.n)
+                HIP_TRY(hipMemsetD32Async(c->d_rot_flags + ch.n, ecdna::ROT_DONE, n_flags - ch.n, st));
+            HIP_TRY(hipMemcpyAsync(c->d_rot_parts, ch.rot_init.data(), ecdna::kRotParts * sizeof(ecdna::RotPart),
+                                   hipMemcpyHostToDevice, st));
         }
 
         HIP_TRY(hipEventRecord(ch.ev[0], st));

@@ -411,6 +411,96 @@ struct BinLayout {
     static constexpr int kSumVecs = (NG + kPerVec - 1) / kPerVec;
 };
 
+// ---- replicate rotation helpers (bin store; DESIGN.md §5 "Rotation")
+//
+// A parked replicate is handed from one CU to another of the SAME XCD (partition = XCC id): the parker's
+// plain stores land in the XCD's L2, it waits for them (vmcnt(0)) before publishing PARKED with an
+// agent-scope atomic, and the resumer reads the state with sc1 loads (vector L1 bypassed, served by that
+// L2) only after its compare-and-swap PARKED -> RUNNING has returned. Flags and counters are only ever
+// read through RMW atomics (compare-and-swap with new == expected, which the compiler cannot turn into a
+// plain load), so a stale cached copy can never hide a waiting replicate.
+constexpr int kCpolSc1 = 16;  // buffer cache policy: sc1 (gfx940+ bit 4)
+
+// Development counters of the rotation (built with -DECDNA_ROT_STATS only; tools/rot_stats.py)
+#ifdef ECDNA_ROT_STATS
+__device__ unsigned long long g_rot_stats[12];
+#define ROT_STAT(i, v) __hip_atomic_fetch_add(&g_rot_stats[i], (unsigned long long)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+#else
+#define ROT_STAT(i, v) ((void)0)
+#endif
+
+// The kernel argument block as seen from a rare path: read through a pointer the compiler cannot prove
+// loop-invariant, so those loads stay inside the rare block instead of holding scalar registers across
+// the event loop (the bin stepper's event path already fills the SGPR file).
+using KArgs = const __attribute__((address_space(4))) StepperArgs;
+__device__ __forceinline__ KArgs* rare_args() {
+    KArgs* p = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
+__device__ __forceinline__ uint4 ld_l2_b128(const void* base, uint32_t byte_off) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff,
+                                                                         0x00020000);
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, kCpolSc1));
+}
+
+// Large-k row cell of a replicate that may have run on another CU of this XCD: vector L1 bypassed
+__device__ __forceinline__ uint32_t gload_u16_l2(const uint16_t* p) {
+    return __hip_atomic_load(const_cast<uint16_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <typename T>
+__device__ __forceinline__ T atomic_read(T* p) {  // memory-side read: CAS(p, 0 -> 0)
+    T e = 0;
+    __hip_atomic_compare_exchange_strong(p, &e, e, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return e;
+}
+
+// Replicate r's state word: from RUNNING (only its owner changes a RUNNING word) to `to`
+__device__ __forceinline__ void rot_set(uint32_t* flags, uint32_t r, uint32_t to) {
+    __hip_atomic_exchange(flags + r, to, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Claim the next waiting replicate of partition `pp` by walking its items one at a time (the lanes of a
+// wave that walk together share one aggregated add on the head): FRESH or PARKED when !fresh_only; FRESH
+// only, and only during the partition's first pass, when fresh_only. The count is checked before the
+// head moves: a lane that has nothing to claim must not consume (and so skip) another lane's item.
+// (C3: per-lane count reads and read-then-CAS 91 ms; one count read per wave round and a blind CAS 88 ms.) Returns 0 when the partition has nothing left to claim, else the state claimed plus one,
+// with the replicate in `out` (chunk-local).
+__device__ __forceinline__ uint32_t rot_claim(KArgs* ra, uint32_t pp, bool fresh_only, uint32_t& out) {
+    RotPart* P = ra->rot_parts + pp;
+    const uint32_t n_pad = ra->rot_n_pad, lo = pp * n_pad;
+    uint32_t* const flags = ra->rot_flags;
+    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+#pragma unroll 1
+    for (;;) {
+        // one read of the count per wave round (the first walking lane), before any item is taken
+        int w = 0;
+        if (lane == __builtin_amdgcn_readfirstlane(lane)) w = atomic_read(fresh_only ? &P->fresh : &P->waiting);
+        if (__builtin_amdgcn_readfirstlane(w) <= 0) return 0u;
+        const unsigned long long j =
+            __hip_atomic_fetch_add(&P->head, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ROT_STAT(fresh_only ? 4 : 1, 1);
+        if (fresh_only && j >= n_pad) return 0u;  // past the first pass: no fresh replicate is left
+        const uint32_t r = lo + (j < (1ull << 32) ? (uint32_t)j % n_pad : (uint32_t)(j % n_pad));
+        // blind compare-and-swap from the likelier waiting state; the value it returns says whether the
+        // item is FRESH after all (one more try) or not waiting (RUNNING / DONE: next item)
+        uint32_t st = fresh_only ? (uint32_t)ROT_FRESH : (uint32_t)ROT_PARKED;
+        if (__hip_atomic_compare_exchange_strong(flags + r, &st, (uint32_t)ROT_RUNNING, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+            (!fresh_only && st == ROT_FRESH &&
+             __hip_atomic_compare_exchange_strong(flags + r, &st, (uint32_t)ROT_RUNNING, __ATOMIC_RELAXED,
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+            __hip_atomic_fetch_add(&P->waiting, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (st == ROT_FRESH) __hip_atomic_fetch_add(&P->fresh, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            out = r;
+            ROT_STAT(st == ROT_FRESH ? 2 : 3, 1);
+            return st + 1u;
+        }
+    }
+}
+
 // Counter j of a 16-B vector (8 x u16 or 4 x u32)
 template <bool C32>
 __device__ __forceinline__ uint32_t vec_get(const uint4& v, int j) {
@@ -529,7 +619,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             for (uint32_t q = 0; q < c; ++q) dst[pos++] = (uint16_t)(b + 1u);
         }
 #pragma unroll 1
-        for (uint32_t j = 0; j < nb; ++j) dst[pos + j] = big[j];
+        for (uint32_t j = 0; j < nb; ++j) dst[pos + j] = (uint16_t)gload_u16_l2(big + j);
     };
 
     // TF: 0 = f64 time and no event hash (compile-time), 1 = both from the runtime flags
@@ -561,22 +651,83 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
     uint32_t stop = 0, err = 0;
     uint32_t sj = 0;
 
-    for (;;) {
-        if (!active) {  // ---- replicate boundary (rare): write the finished one, pull the next
-            if (have) {
-                // final bin counters -> bags[li] (B stays in the row)
-                uint4* bag = reinterpret_cast<uint4*>(a.bags) + (uint64_t)li * L::kBinVecs;
-                if (C32) {
+    // bin counters of the lane's replicate -> bags[li] (final, or parked); B stays in the row
+    auto store_bag = [&]() {
+        uint4* bag = reinterpret_cast<uint4*>(rare_args()->bags) + (uint64_t)li * L::kBinVecs;
+        if (C32) {
 #pragma unroll 8
-                    for (uint32_t v = 0; v < (uint32_t)L::kBinVecs; ++v) {
-                        const uint32_t* c = cnt_w + 4u * v * BLK + tid;
-                        bag[v] = make_uint4(c[0], c[BLK], c[2 * BLK], c[3 * BLK]);
-                    }
-                } else {
+            for (uint32_t v = 0; v < (uint32_t)L::kBinVecs; ++v) {
+                const uint32_t* c = cnt_w + 4u * v * BLK + tid;
+                bag[v] = make_uint4(c[0], c[BLK], c[2 * BLK], c[3 * BLK]);
+            }
+        } else {
 #pragma unroll
-                    for (int v = 0; v < L::kBinVecs; ++v) bag[v] = cnt_v[v][tid];
+            for (int v = 0; v < L::kBinVecs; ++v) bag[v] = cnt_v[v][tid];
+        }
+    };
+
+    // Replicate rotation (a.rot_parts != nullptr): every 2^rot_tick_log2 loop iterations
+    // (a wave-uniform tick) the wave parks its lanes' replicates if enough others of its XCD's partition
+    // wait, and the lanes claim waiting ones in the partition's round-robin item order. A lane whose
+    // partition has nothing left takes fresh replicates of other partitions and runs them to their end
+    // without parking ("pinned": their state never crosses an XCD).
+    const bool rot = a.rot_parts != nullptr;  // (kept: the tick test reads it every iteration)
+    unsigned xcc_id;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_id));
+    const uint32_t part = xcc_id % kRotParts;
+    const uint32_t tick_mask = rot ? ((1u << a.rot_tick_log2) - 1u) : 0xffffffffu;
+    uint32_t it = 0;
+    bool pinned = false;
+
+#ifdef ECDNA_ROT_STATS
+    unsigned long long c_tick = 0, c_bound = 0, c_start = clock64();
+#endif
+    for (;;) {
+        if (rot && ((++it & tick_mask) == 0u)) {  // ---- rotation tick (wave-uniform)
+#ifdef ECDNA_ROT_STATS
+            const unsigned long long c0 = clock64();
+#endif
+            KArgs* const ra = rare_args();
+            RotPart* P = ra->rot_parts + part;
+            const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+            int w = 0;
+            if (lane == __builtin_amdgcn_readfirstlane(lane)) w = atomic_read(&P->waiting);
+            w = __builtin_amdgcn_readfirstlane(w);
+            ROT_STAT(w >= ra->rot_park_min ? 5 : 6, 1);
+            if (w >= ra->rot_park_min) {
+                const bool pk = active && !pinned;
+                if (pk) {
+                    store_bag();
+                    uint4* q = ra->rot_park + (uint64_t)li * kParkVecs;
+                    q[0] = make_uint4(nm, ns, nb, e);
+                    q[1] = make_uint4(sp0, sp1, nsp, sj);
+                    q[2] = make_uint4(n_dm, n_un, np0, nm0);
+                    const uint64_t tb = f32t ? (uint64_t)__float_as_uint(t32) : (uint64_t)__double_as_longlong(t);
+                    q[3] = make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), (uint32_t)h, (uint32_t)(h >> 32));
                 }
-                ecdna_rep_summary_t* s = a.summaries + li;
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the state is in the XCD's L2
+                if (pk) {
+                    __hip_atomic_fetch_add(&P->waiting, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // counted before it can be claimed
+                    rot_set(ra->rot_flags, li, ROT_PARKED);
+                    ROT_STAT(0, 1);
+                    active = false;
+                    have = false;
+                }
+            }
+#ifdef ECDNA_ROT_STATS
+            c_tick += clock64() - c0;
+#endif
+        }
+#ifdef ECDNA_ROT_STATS
+        const unsigned long long cb0 = clock64();
+        const bool any_bound = __builtin_amdgcn_read_exec() & __ballot(!active);
+#endif
+        if (!active) {  // ---- replicate boundary (rare): write the finished one, pull the next
+            KArgs* const ra = rare_args();
+            if (have) {
+                store_bag();
+                ecdna_rep_summary_t* s = ra->summaries + li;
                 s->nminus = nm;
                 s->nplus = ns + nb;
                 s->iters = e;
@@ -596,59 +747,132 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                 s->event_hash = hash_on ? h : 0ull;
                 s->stop_reason = stop;
                 s->error = err;
+                if (rot) rot_set(ra->rot_flags, li, ROT_DONE);
+                have = false;
             }
-            if (young && __hip_atomic_load(a.head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + a.admit_remaining >= a.n)
-                break;
-            const uint32_t i = atomicAdd(a.head, 1u);
-            if (i >= a.n) break;
+            uint32_t i = 0, kind = ROT_FRESH + 1u;
+            if (rot) {
+                kind = rot_claim(ra, part, false, i);
+                pinned = false;
+#pragma unroll 1
+                for (uint32_t d = 1; kind == 0u && d < kRotParts; ++d) {  // own partition drained: steal fresh
+                    kind = rot_claim(ra, (part + d) % kRotParts, true, i);
+                    pinned = kind != 0u;
+                }
+                if (kind == 0u) break;
+            } else {
+                if (young &&
+                    __hip_atomic_load(ra->head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + ra->admit_remaining >= ra->n)
+                    break;
+                i = atomicAdd(ra->head, 1u);
+                if (i >= ra->n) break;
+            }
             have = true;
             active = true;
             li = i;
-            rid = a.rid0 + i;
+            rid = ra->rid0 + i;
             pre = philox_event_pre((uint32_t)rid, (uint32_t)(rid >> 32), rk);
-            row = a.rows + (uint64_t)i * a.row_stride;
-            const uint64_t set = rid / a.reps_per_set;
-            const float4 r = a.rates[set];
+            row = ra->rows + (uint64_t)i * ra->row_stride;
+            const uint64_t set = rid / ra->reps_per_set;
+            const float4 r = ra->rates[set];
             rb0 = (double)r.x;
             rb1 = (double)r.y;
             rd0 = (double)r.z;
             rd1 = (double)r.w;
-            const uint16_t* src = a.init_copies;
-            uint32_t cnt = a.init_nplus;
-            if (a.init_offsets) {
-                src = a.init_copies + a.init_offsets[set];
-                cnt = a.init_offsets[set + 1] - a.init_offsets[set];
-            }
-            bins_zero();
-            ns = 0;
-            nb = 0;
-#pragma unroll 1
-            for (uint32_t j = 0; j < cnt; ++j) {
-                const uint32_t kk = src[j];
-                if (kk <= K) {
-                    bin_add(kk, 1u);
-                    ++ns;
-                } else {
-                    row[nb++] = (uint16_t)kk;
-                }
-            }
-            nm = (uint32_t)(a.init_nminus_set ? a.init_nminus_set[set] : a.init_nminus);
-            t = 0.0;
-            t32 = 0.f;
-            e = n_dm = n_un = 0;
-            np0 = ns + nb;
-            nm0 = nm;
-            nsp = 0;
-            h = kFnvOffset;
             stop = 0;
             err = 0;
-            sj = 0;
-            if (ns + nb == 0 && nm == 0) {  // ensure!(!distribution.is_empty()) src/process.rs:88, 232
-                err = ECDNA_REP_ERR_EMPTY;
-                stop = ECDNA_STOP_ERROR;
-                active = false;
+            if (kind == ROT_PARKED + 1u) {  // resume: the parker's stores, through the XCD's L2
+                const uint32_t bag_bytes = (uint32_t)(L::kBinVecs * 16);
+#pragma unroll 1
+                for (uint32_t v = 0; v < (uint32_t)L::kBinVecs; ++v) {
+                    const uint4 c = ld_l2_b128(ra->bags, i * bag_bytes + v * 16u);
+                    if (C32) {
+                        uint32_t* d = cnt_w + 4u * v * BLK + tid;
+                        d[0] = c.x;
+                        d[BLK] = c.y;
+                        d[2 * BLK] = c.z;
+                        d[3 * BLK] = c.w;
+                    } else {
+                        cnt_v[v][tid] = c;
+                    }
+                }
+                if (C32) {
+#pragma unroll 1
+                    for (uint32_t g = 0; g < (uint32_t)NG; ++g) {
+                        uint32_t sg = 0;
+#pragma unroll
+                        for (uint32_t b = 0; b < 8u; ++b) sg += cnt_w[(8u * g + b) * BLK + tid];
+                        sum_w[g * BLK + tid] = sg;
+                    }
+                } else {
+#pragma unroll
+                    for (int v = 0; v < L::kSumVecs; ++v) sum_v[v][tid] = make_uint4(0, 0, 0, 0);
+#pragma unroll 1
+                    for (uint32_t g = 0; g < (uint32_t)NG; ++g) {
+                        uint32_t sg = 0;
+#pragma unroll
+                        for (uint32_t b = 8u * g; b < 8u * g + 8u; ++b) sg += (*bin_word(b) >> ((b & 1u) * 16)) & 0xffffu;
+                        atomicAdd(sum_w + word_index(g), shifted(g, sg));
+                    }
+                }
+                const uint32_t pb = i * (uint32_t)(kParkVecs * 16);
+                const uint4 q0 = ld_l2_b128(ra->rot_park, pb), q1 = ld_l2_b128(ra->rot_park, pb + 16u);
+                const uint4 q2 = ld_l2_b128(ra->rot_park, pb + 32u), q3 = ld_l2_b128(ra->rot_park, pb + 48u);
+                nm = q0.x;
+                ns = q0.y;
+                nb = q0.z;
+                e = q0.w;
+                sp0 = q1.x;
+                sp1 = q1.y;
+                nsp = q1.z;
+                sj = q1.w;
+                n_dm = q2.x;
+                n_un = q2.y;
+                np0 = q2.z;
+                nm0 = q2.w;
+                const uint64_t tb = (uint64_t)q3.x | ((uint64_t)q3.y << 32);
+                t = f32t ? 0.0 : __longlong_as_double((long long)tb);
+                t32 = f32t ? __uint_as_float((uint32_t)tb) : 0.f;
+                h = (uint64_t)q3.z | ((uint64_t)q3.w << 32);
+            } else {
+                const uint16_t* src = ra->init_copies;
+                uint32_t cnt = ra->init_nplus;
+                if (ra->init_offsets) {
+                    src = ra->init_copies + ra->init_offsets[set];
+                    cnt = ra->init_offsets[set + 1] - ra->init_offsets[set];
+                }
+                bins_zero();
+                ns = 0;
+                nb = 0;
+#pragma unroll 1
+                for (uint32_t j = 0; j < cnt; ++j) {
+                    const uint32_t kk = src[j];
+                    if (kk <= K) {
+                        bin_add(kk, 1u);
+                        ++ns;
+                    } else {
+                        row[nb++] = (uint16_t)kk;
+                    }
+                }
+                nm = (uint32_t)(ra->init_nminus_set ? ra->init_nminus_set[set] : ra->init_nminus);
+                t = 0.0;
+                t32 = 0.f;
+                e = n_dm = n_un = 0;
+                np0 = ns + nb;
+                nm0 = nm;
+                nsp = 0;
+                h = kFnvOffset;
+                sj = 0;
+                if (ns + nb == 0 && nm == 0) {  // ensure!(!distribution.is_empty()) src/process.rs:88, 232
+                    err = ECDNA_REP_ERR_EMPTY;
+                    stop = ECDNA_STOP_ERROR;
+                    active = false;
+                }
             }
         }
+#ifdef ECDNA_ROT_STATS
+        if (any_bound) c_bound += clock64() - cb0;
+#endif
         if (!active) continue;  // (an empty initial distribution)
         const uint32_t np = ns + nb;
 
@@ -722,7 +946,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             const uint32_t idx = (uint32_t)(m >> 32);
             const bool small = idx < ns;
             uint32_t k = bin_find(small ? idx : 0u);
-            if (nplus_ev && !small) k = gload_u16(row + (idx - ns));  // large-k row (rare)
+            if (nplus_ev && !small) k = gload_u16_l2(row + (idx - ns));  // large-k row (rare)
 
             // Exponential::increase_nplus (src/proliferation.rs:25-111): its draws and error checks
             const uint32_t n = 2u * k;
@@ -806,7 +1030,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                         }
                     }
                     if (open != 0xffffffffu) {  // swap_remove(open) from B
-                        if (open != nb - 1) row[open] = (uint16_t)gload_u16(row + nb - 1);
+                        if (open != nb - 1) row[open] = (uint16_t)gload_u16_l2(row + nb - 1);
                         nb -= 1;
                     }
                 }
@@ -827,6 +1051,13 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             }
         }
     }
+#ifdef ECDNA_ROT_STATS
+    if ((threadIdx.x & 63u) == 0u) {
+        ROT_STAT(8, c_tick);
+        ROT_STAT(9, c_bound);
+        ROT_STAT(10, clock64() - c_start);
+    }
+#endif
 }
 
 __device__ __forceinline__ void wave_sync_lds() {
@@ -1050,3 +1281,12 @@ hipError_t launch_hist(const HistArgs& a, uint32_t blocks, hipStream_t stream) {
 }
 
 }  // namespace ecdna
+
+#ifdef ECDNA_ROT_STATS
+// Development: read (and reset) the rotation counters of the last launches (tools/rot_stats.py)
+extern "C" int ecdna_dev_rot_stats(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ecdna::g_rot_stats), sizeof(ecdna::g_rot_stats)) != hipSuccess) return -1;
+    unsigned long long z[12] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(ecdna::g_rot_stats), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

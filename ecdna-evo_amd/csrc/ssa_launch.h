@@ -9,6 +9,21 @@
 
 namespace ecdna {
 
+// Replicate rotation (bin store): replicates are split into kRotParts partitions, one per XCD (the
+// XCC id of the lane's CU), so a parked replicate is only ever resumed by a CU that shares the L2 it
+// was parked through. A partition's waiting replicates are found by walking its items: item j is
+// replicate lo + j % rot_n_pad (pass j / rot_n_pad: round-robin order); rot_n_pad is a multiple of kRotBlock.
+constexpr uint32_t kRotParts = 8;
+constexpr uint32_t kRotBlock = 16;
+constexpr uint32_t kParkVecs = 4;    // 64 B of scalars per parked replicate
+enum RotState : uint32_t { ROT_FRESH = 0, ROT_RUNNING = 1, ROT_PARKED = 2, ROT_DONE = 3 };
+struct alignas(128) RotPart {
+    unsigned long long head;        // items walked
+    int waiting;                    // FRESH + PARKED replicates (never below the number of such flags)
+    int fresh;                      // FRESH replicates
+    uint32_t pad[28];
+};
+
 // One chunk of replicates for the persistent SSA stepper.
 struct StepperArgs {
     uint16_t* rows;                 // [n][row_stride] per-replicate N+ rows (replicate-major)
@@ -42,6 +57,16 @@ struct StepperArgs {
     // replicate once fewer than admit_remaining are left; admit_slot = 0xffffffff: off
     uint32_t admit_slot;
     uint32_t admit_remaining;
+    // bin store replicate rotation ("Rotation"): every 2^rot_tick_log2 loop iterations a
+    // wave parks its lanes' replicates (bin counters -> bags, scalars -> park) and its lanes pull the next
+    // waiting replicate of their XCD's partition, so all replicates advance together and none starts
+    // late. rot_parts = nullptr: off.
+    RotPart* rot_parts;             // [kRotParts] (host-initialised per launch)
+    uint32_t* rot_flags;            // [kRotParts * rot_n_pad]: RotState per replicate
+    uint4* rot_park;                // [n][kParkVecs] parked scalars
+    uint32_t rot_n_pad;             // replicates per partition, multiple of kRotBlock
+    uint32_t rot_tick_log2;
+    int32_t rot_park_min;           // park at a tick only if at least this many replicates wait
 };
 
 // Histogram / totals pass over one chunk.
