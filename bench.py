@@ -161,6 +161,7 @@ def main():
     ap.add_argument("--reps-per-gpu", type=int, default=REPS_PER_GPU)
     ap.add_argument("--store", choices=("bins", "rows"), default="bins")
     ap.add_argument("--bin-kmax", type=int, choices=(32, 64, 256), default=BENCH_BIN_KMAX)
+    ap.add_argument("--dump-hist", default="", help="rank 0 saves the reduced histogram and totals (.npz)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -168,9 +169,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # under torchrun (even at one rank) the RCCL path runs: process group, all-reduce, barriers
     distributed = "RANK" in os.environ and "MASTER_ADDR" in os.environ
+    # rehearsal knobs for a one-GPU box (tests/test_gpu_bench_dist.py): every rank on cuda:0, reduced over
+    # gloo (RCCL refuses two ranks on one device); the driver's runs use neither
+    backend = os.environ.get("ECDNA_BENCH_BACKEND", "nccl")
+    if os.environ.get("ECDNA_BENCH_ONE_DEVICE") == "1":
+        local = 0
     if distributed:
         torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend=backend)
     else:
         torch.cuda.set_device(0)
     n_gpus = world
@@ -231,6 +240,10 @@ def main():
     assert int(tot_host[0]) == total, f"all-reduced totals count {int(tot_host[0])} replicates, expected {total}"
     assert int(tot_host[1]) == events_per_step
 
+    if rank == 0 and args.dump_hist:
+        import numpy as np
+
+        np.savez(args.dump_hist, hist=hist.cpu().numpy(), totals=tot_host)
     if rank == 0:
         avg_kernel_s = sum(kernel_ms) / len(kernel_ms) * 1e-3
         achieved = local_alg / avg_kernel_s / 1e9

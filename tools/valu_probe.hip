@@ -152,6 +152,65 @@ OPKERNEL(k_lshl_add_u64, uint64_t, 1, "v_lshl_add_u64 %0, %0, 1, %1", "v", uint6
 OPKERNEL(k_mul_f64, double, 0.5, "v_mul_f64 %0, %0, %1", "v", double)
 OPKERNEL(k_cvt_f32_u32, float, 1, "v_cvt_f32_u32 %0, %1", "v", uint32_t)
 OPKERNEL(k_rcp_f64, double, 1, "v_rcp_f64 %0, %1", "v", double)
+// round 2: encodings and operand kinds of the stepper's instruction mix
+OPKERNEL(k_ashr_v, uint32_t, 1, "v_ashrrev_i32 %0, %1, %0", "v", uint32_t)
+OPKERNEL(k_bitop3, uint32_t, 1, "v_bitop3_b32 %0, %0, %1, %1 bitop3:0x96", "v", uint32_t)
+OPKERNEL(k_lshl_or, uint32_t, 1, "v_lshl_or_b32 %0, %0, 3, %1", "v", uint32_t)
+OPKERNEL(k_perm, uint32_t, 1, "v_perm_b32 %0, %0, %1, %1", "v", uint32_t)
+OPKERNEL(k_add_e64, uint32_t, 1, "v_add_u32_e64 %0, %0, %1", "v", uint32_t)
+OPKERNEL(k_xor_e64, uint32_t, 1, "v_xor_b32_e64 %0, %0, %1", "v", uint32_t)
+OPKERNEL(k_lshr_e64, uint32_t, 1, "v_lshrrev_b32_e64 %0, %1, %0", "v", uint32_t)
+OPKERNEL(k_lshl_imm, uint32_t, 1, "v_lshlrev_b32 %0, 3, %0", "v", uint32_t)
+OPKERNEL(k_mul_f64_s, double, 0.5, "v_mul_f64 %0, %0, %1", "s", double)
+OPKERNEL(k_add_f64_v, double, 0.5, "v_add_f64 %0, %0, %1", "v", double)
+OPKERNEL(k_cvt_f64_i32, double, 1, "v_cvt_f64_i32 %0, %1", "v", uint32_t)
+OPKERNEL(k_min3, uint32_t, 1, "v_min3_u32 %0, %0, %1, %1", "v", uint32_t)
+OPKERNEL(k_sub_co, uint32_t, 1, "v_sub_co_u32 %0, vcc, %0, %1", "v", uint32_t)
+OPKERNEL(k_add_lit, uint32_t, 1, "v_add_u32 %0, 0x12345, %0", "v", uint32_t)
+
+__global__ void __launch_bounds__(256) k_mad_u64_v(uint32_t* out, uint32_t s) {
+    uint64_t v[8];
+    const uint32_t c = s + threadIdx.x * 0u;  // the constant in a VGPR
+    uint32_t cv;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(cv) : "s"(c));
+    for (int j = 0; j < 8; ++j) v[j] = threadIdx.x + j;
+    for (int i = 0; i < ITERS; ++i) {
+        _Pragma("unroll") for (int j = 0; j < 8; ++j)
+            asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(v[j]) : "v"((uint32_t)v[j]), "v"(cv) : "vcc");
+    }
+    uint64_t r = 0;
+    for (int j = 0; j < 8; ++j) r ^= v[j];
+    if (r == 0x12345) out[0] = (uint32_t)r;
+}
+
+// v_cndmask_b32_e64 with an SGPR-pair condition (the compiler's usual select form)
+__global__ void __launch_bounds__(256) k_cndmask_s(uint32_t* out, uint32_t s) {
+    uint32_t v[8];
+    uint64_t m = (s & 1u) ? 0x5555aaaa5555ull : 0x5555ull;
+    asm volatile("" : "+s"(m));
+    for (int j = 0; j < 8; ++j) v[j] = threadIdx.x + j;
+    for (int i = 0; i < ITERS; ++i) {
+        _Pragma("unroll") for (int j = 0; j < 8; ++j)
+            asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(v[j]) : "v"(s), "s"(m));
+    }
+    uint32_t r = 0;
+    for (int j = 0; j < 8; ++j) r ^= v[j];
+    if (r == 0x12345) out[0] = r;
+}
+
+// v_cmp_gt_u32_e64 into an SGPR pair (8 independent compares per lane per iteration)
+__global__ void __launch_bounds__(256) k_cmp_s(uint32_t* out, uint32_t s) {
+    uint32_t v[8];
+    uint64_t m[8];
+    for (int j = 0; j < 8; ++j) v[j] = threadIdx.x + j;
+    for (int i = 0; i < ITERS; ++i) {
+        _Pragma("unroll") for (int j = 0; j < 8; ++j)
+            asm volatile("v_cmp_gt_u32_e64 %0, %1, %2" : "=s"(m[j]) : "v"(v[j]), "v"(s));
+    }
+    uint64_t r = 0;
+    for (int j = 0; j < 8; ++j) r ^= m[j];
+    if (r == 0x12345) out[0] = 1;
+}
 
 template <typename F>
 void time_it(const char* name, F launch, double insts_per_lane_iter, int cus, double clk_hz) {
@@ -217,5 +276,22 @@ int main() {
     time_it("cvt_f32_u32", [&] { hipLaunchKernelGGL(k_cvt_f32_u32, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
     time_it("rcp_f64", [&] { hipLaunchKernelGGL(k_rcp_f64, g, blk, 0, 0, d, 0.5); }, 8, cus, clk);
     time_it("ds_add_u32", [&] { hipLaunchKernelGGL(k_ds_add, g, blk, 0, 0, d, 1u); }, 8, cus, clk);
+    time_it("ashrrev_v", [&] { hipLaunchKernelGGL(k_ashr_v, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
+    time_it("bitop3_v", [&] { hipLaunchKernelGGL(k_bitop3, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
+    time_it("lshl_or_v", [&] { hipLaunchKernelGGL(k_lshl_or, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
+    time_it("perm_v", [&] { hipLaunchKernelGGL(k_perm, g, blk, 0, 0, d, 0x05040100u); }, 8, cus, clk);
+    time_it("add_u32_e64_v", [&] { hipLaunchKernelGGL(k_add_e64, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
+    time_it("xor_e64_v", [&] { hipLaunchKernelGGL(k_xor_e64, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
+    time_it("lshrrev_e64_v", [&] { hipLaunchKernelGGL(k_lshr_e64, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
+    time_it("lshlrev_imm", [&] { hipLaunchKernelGGL(k_lshl_imm, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
+    time_it("mul_f64_s", [&] { hipLaunchKernelGGL(k_mul_f64_s, g, blk, 0, 0, d, 0.5); }, 8, cus, clk);
+    time_it("add_f64_v", [&] { hipLaunchKernelGGL(k_add_f64_v, g, blk, 0, 0, d, 0.5); }, 8, cus, clk);
+    time_it("cvt_f64_i32", [&] { hipLaunchKernelGGL(k_cvt_f64_i32, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
+    time_it("min3_u32", [&] { hipLaunchKernelGGL(k_min3, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
+    time_it("sub_co_vcc", [&] { hipLaunchKernelGGL(k_sub_co, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
+    time_it("add_lit", [&] { hipLaunchKernelGGL(k_add_lit, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
+    time_it("mad_u64_v", [&] { hipLaunchKernelGGL(k_mad_u64_v, g, blk, 0, 0, d, 0xD2511F53u); }, 8, cus, clk);
+    time_it("cndmask_e64_s", [&] { hipLaunchKernelGGL(k_cndmask_s, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
+    time_it("cmp_e64_s", [&] { hipLaunchKernelGGL(k_cmp_s, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
     return 0;
 }
