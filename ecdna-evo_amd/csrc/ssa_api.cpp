@@ -71,7 +71,10 @@ int validate(const ecdna_ssa_params_t* p) {
     if (p->segregation < 0 || p->segregation > 3) return fail(ECDNA_E_INVALID, "unknown segregation");
     if (p->max_iter > 0xffffffffull) return fail(ECDNA_E_INVALID, "max_iter must be < 2^32");
     if (p->n_replicates > 0xffffffffull) return fail(ECDNA_E_INVALID, "n_replicates must be < 2^32 per call");
-    if (p->n_replicates && (p->first_replicate + p->n_replicates - 1) / p->reps_per_set >= p->n_param_sets)
+    const uint64_t stride = p->replicate_stride ? p->replicate_stride : 1u;
+    if (p->n_replicates && (p->n_replicates - 1) > (~0ull - p->first_replicate) / stride)
+        return fail(ECDNA_E_INVALID, "replicate ids overflow u64");
+    if (p->n_replicates && (p->first_replicate + (p->n_replicates - 1) * stride) / p->reps_per_set >= p->n_param_sets)
         return fail(ECDNA_E_INVALID, "replicate ids map past the last parameter set");
     if (p->cell_cap == 0) return fail(ECDNA_E_INVALID, "cell_cap must be >= 1");
     if ((p->flags & ECDNA_FLAG_BIN_STORE) && p->bin_kmax != 0 && p->bin_kmax != 32 && p->bin_kmax != 64 &&
@@ -425,8 +428,7 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
         ch.rot_n_pad = (per + ecdna::kRotBlock - 1) / ecdna::kRotBlock * ecdna::kRotBlock;
         ch.rot_init.assign(ecdna::kRotParts, ecdna::RotPart{});
         for (uint32_t x = 0; x < ecdna::kRotParts; ++x) {
-            const uint64_t lo = (uint64_t)x * ch.rot_n_pad, hi = std::min<uint64_t>(lo + ch.rot_n_pad, ch.n);
-            const int cnt = hi > lo ? (int)(hi - lo) : 0;
+            const int cnt = x < ch.n ? (int)((ch.n - x + ecdna::kRotParts - 1) / ecdna::kRotParts) : 0;  // r = x mod 8
             ch.rot_init[x].waiting = cnt;
             ch.rot_init[x].fresh = cnt;
         }
@@ -480,7 +482,9 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
         a.init_nminus_set = c->d_init_nm;
         a.row_stride = c->row_stride;
         a.seed = p.seed;
-        a.rid0 = p.first_replicate + ch.first;
+        const uint64_t stride = p.replicate_stride ? p.replicate_stride : 1u;
+        a.rid0 = p.first_replicate + ch.first * stride;
+        a.rid_stride = stride;
         a.reps_per_set = p.reps_per_set;
         a.max_cells = p.max_cells;
         a.init_nminus = p.init_nminus;
@@ -545,7 +549,8 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
         hsa.hist = c->d_hist;
         hsa.totals = reinterpret_cast<unsigned long long*>(c->d_tot);
         hsa.row_stride = c->row_stride;
-        hsa.rid0 = p.first_replicate + ch.first;
+        hsa.rid0 = p.first_replicate + ch.first * stride;
+        hsa.rid_stride = stride;
         hsa.reps_per_set = p.reps_per_set;
         hsa.n = ch.n;
         hsa.bins = p.hist_bins;

@@ -184,14 +184,40 @@ struct WordStream {
         return sel((q & 2u) != 0, sel(odd, blk.w, blk.z), sel(odd, blk.y, blk.x));
     }
 
-    // popcount of the next n stream bits (n >= 1): k1 ~ Binomial(n, 1/2) exactly.
-    __device__ __forceinline__ uint32_t binomial_half(uint32_t n) {
+    // the low `take` bits (0 <= take <= 32)
+    static __device__ __forceinline__ uint32_t low_bits(uint32_t take) { return (uint32_t)((1ull << take) - 1ull); }
+
+    // popcount of the next n stream bits (n >= 1): k1 ~ Binomial(n, 1/2) exactly. The same words in the
+    // same order as ceil(n / 32) calls of next() (the low bits of the last one), but past the base words
+    // and spares the Philox blocks come from a lane-uniform loop, one block per iteration with its four
+    // words popcounted branch-free. (Word by word, next() generates a block whenever ANY lane of the
+    // wave crosses a block boundary, and lanes sit at different stream offsets: large copy numbers then
+    // ran a Philox block for almost every word. rk: the kernel's VGPR round keys, or nullptr.)
+    __device__ __forceinline__ uint32_t binomial_half(uint32_t n, const PhiloxKeys* rk = nullptr) {
         uint32_t c = 0;
-        while (n >= 32) {
-            c += __popc(next());
-            n -= 32;
+        while (n && pos < 2u + nsp) {  // w3 and the spares (at most three words; no Philox block here)
+            const uint32_t p = pos++;
+            const uint32_t w = p < 2u ? sel(p == 0u, w2, w3) : sel(p == 2u, s0, s1);
+            const uint32_t take = min(n, 32u);
+            c += __popc(w & low_bits(take));
+            n -= take;
         }
-        if (n) c += __popc(next() & ((1u << n) - 1u));
+        while (n) {
+            const uint32_t q = pos - 2u - nsp;  // stream offset inside the block region
+            const uint32_t j = (q >> 2) + 1u;
+            const uint4 c4 = make_uint4(e, j, rid_lo, rid_hi);
+            blk = rk ? philox4x32_10(c4, *rk) : philox4x32_10(c4, k0, k1);
+            blk_id = j;
+            const uint32_t t0 = q & 3u;
+            const uint32_t w[4] = {blk.x, blk.y, blk.z, blk.w};
+#pragma unroll
+            for (uint32_t t = 0; t < 4u; ++t) {
+                const uint32_t take = t >= t0 ? min(n, 32u) : 0u;
+                c += __popc(w[t] & low_bits(take));
+                n -= take;
+                pos += take ? 1u : 0u;
+            }
+        }
         return c;
     }
 };

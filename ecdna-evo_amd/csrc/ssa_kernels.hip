@@ -146,7 +146,7 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
             have = true;
             active = true;
             li = i;
-            rid = a.rid0 + i;
+            rid = a.rid0 + (uint64_t)i * a.rid_stride;
             row = a.rows + (uint64_t)i * a.row_stride;
             const uint64_t set = rid / a.reps_per_set;
             const float4 r = a.rates[set];
@@ -470,7 +470,7 @@ __device__ __forceinline__ void rot_set(uint32_t* flags, uint32_t r, uint32_t to
 // with the replicate in `out` (chunk-local).
 __device__ __forceinline__ uint32_t rot_claim(KArgs* ra, uint32_t pp, bool fresh_only, uint32_t& out) {
     RotPart* P = ra->rot_parts + pp;
-    const uint32_t n_pad = ra->rot_n_pad, lo = pp * n_pad;
+    const uint32_t n_pad = ra->rot_n_pad;
     uint32_t* const flags = ra->rot_flags;
     const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 #pragma unroll 1
@@ -483,7 +483,9 @@ __device__ __forceinline__ uint32_t rot_claim(KArgs* ra, uint32_t pp, bool fresh
             __hip_atomic_fetch_add(&P->head, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ROT_STAT(fresh_only ? 4 : 1, 1);
         if (fresh_only && j >= n_pad) return 0u;  // past the first pass: no fresh replicate is left
-        const uint32_t r = lo + (j < (1ull << 32) ? (uint32_t)j % n_pad : (uint32_t)(j % n_pad));
+        // partitions interleave the replicates (r mod kRotParts), so a run whose cost varies along the
+        // replicate order (an ABC sweep's parameter sets) gives every XCD the same mix
+        const uint32_t r = pp + kRotParts * (j < (1ull << 32) ? (uint32_t)j % n_pad : (uint32_t)(j % n_pad));
         // blind compare-and-swap from the likelier waiting state; the value it returns says whether the
         // item is FRESH after all (one more try) or not waiting (RUNNING / DONE: next item)
         uint32_t st = fresh_only ? (uint32_t)ROT_FRESH : (uint32_t)ROT_PARKED;
@@ -770,7 +772,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             have = true;
             active = true;
             li = i;
-            rid = ra->rid0 + i;
+            rid = ra->rid0 + (uint64_t)i * ra->rid_stride;
             pre = philox_event_pre((uint32_t)rid, (uint32_t)(rid >> 32), rk);
             row = ra->rows + (uint64_t)i * ra->row_stride;
             const uint64_t set = rid / ra->reps_per_set;
@@ -963,7 +965,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                 k1v = __popc(w.w & (uint32_t)m64) + __popc(sp0 & (uint32_t)(m64 >> 32));
                 if (prolif && fast) ws.pos = fast1 ? 2u : 3u;
                 if (prolif && !fast && k <= 32767u) {  // larger copy numbers or a rejected pick: more words
-                    k1v = ws.binomial_half(n);
+                    k1v = ws.binomial_half(n, &rk);
                     if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN) {
                         uint32_t tries = 1;
                         while (k1v == 0u || k1v == n) {
@@ -971,7 +973,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                                 ev_err = ECDNA_REP_ERR_REJECTION;
                                 break;
                             }
-                            k1v = ws.binomial_half(n);
+                            k1v = ws.binomial_half(n, &rk);
                             ++tries;
                         }
                     }
@@ -982,7 +984,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                             ev_err = ECDNA_REP_ERR_REJECTION;
                             break;
                         }
-                        k1v = ws.binomial_half(n);
+                        k1v = ws.binomial_half(n, &rk);
                         ++tries;
                     }
                 }
@@ -1101,9 +1103,11 @@ __global__ void __launch_bounds__(kHistBlock) ssa_hist(const HistArgs a) {
 
     uint32_t r = r_begin;
     while (r < r_end) {
-        const uint64_t set = (a.rid0 + r) / a.reps_per_set;
+        // local replicates r .. seg_end - 1 share a parameter set: ids rid0 + r * stride below set_end_rid
+        const uint64_t set = (a.rid0 + (uint64_t)r * a.rid_stride) / a.reps_per_set;
         const uint64_t set_end_rid = (set + 1) * a.reps_per_set;
-        const uint32_t seg_end = (uint32_t)min((uint64_t)r_end, set_end_rid - a.rid0);
+        const uint64_t in_set = (set_end_rid - a.rid0 + a.rid_stride - 1) / a.rid_stride;
+        const uint32_t seg_end = (uint32_t)min((uint64_t)r_end, in_set);
         for (uint32_t b = tid; b < a.bins + 16; b += blockDim.x) lds[b] = 0ull;
         __syncthreads();
         for (uint32_t q = r + wave; q < seg_end; q += nw) {

@@ -11,8 +11,9 @@ namespace ecdna {
 
 // Replicate rotation (bin store): replicates are split into kRotParts partitions, one per XCD (the
 // XCC id of the lane's CU), so a parked replicate is only ever resumed by a CU that shares the L2 it
-// was parked through. A partition's waiting replicates are found by walking its items: item j is
-// replicate lo + j % rot_n_pad (pass j / rot_n_pad: round-robin order); rot_n_pad is a multiple of kRotBlock.
+// was parked through. Partition x holds the replicates r with r mod kRotParts == x; its waiting
+// replicates are found by walking its items: item j is replicate x + kRotParts * (j % rot_n_pad) (pass
+// j / rot_n_pad: round-robin order; slots past the chunk are DONE); rot_n_pad is a multiple of kRotBlock.
 constexpr uint32_t kRotParts = 8;
 constexpr uint32_t kRotBlock = 16;
 constexpr uint32_t kParkVecs = 4;    // 64 B of scalars per parked replicate
@@ -36,6 +37,7 @@ struct StepperArgs {
     uint64_t row_stride;            // cells per row (multiple of 64 -> 128-B aligned rows)
     uint64_t seed;
     uint64_t rid0;                  // global id of the chunk's first replicate
+    uint64_t rid_stride;            // global-id step between the chunk's replicates (>= 1)
     uint64_t reps_per_set;
     uint64_t max_cells;
     uint64_t stop_cells;            // MaxCells when n- + n+ >= stop_cells: max_cells, or
@@ -77,6 +79,7 @@ struct HistArgs {
     unsigned long long* totals;           // [n_sets][16] (ecdna_totals_t as u64 words)
     uint64_t row_stride;
     uint64_t rid0;
+    uint64_t rid_stride;                  // >= 1
     uint64_t reps_per_set;
     uint32_t n;
     uint32_t bins;

@@ -14,7 +14,7 @@ from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # ecdna_process_t (ProcessType, src/clap_app.rs:311-315)
 PURE_BIRTH = 0
@@ -84,7 +84,7 @@ class Params(C.Structure):
         ("reserved1", C.c_int32),
         ("snapshot_cells", C.POINTER(C.c_uint64)),
         ("n_snapshots", C.c_uint32),
-        ("reserved2", C.c_uint32),
+        ("replicate_stride", C.c_uint32),
         ("stats_target_hist", C.POINTER(C.c_uint64)),
     ]
 
@@ -158,6 +158,7 @@ class RunSpec:
     seed: int = 26  # src/clap_app.rs:63
     first_replicate: int = 0
     n_replicates: int = 12  # src/clap_app.rs:89
+    replicate_stride: int = 1  # replicate i has global id first_replicate + i * replicate_stride
     max_cells: int = 1000  # src/clap_app.rs:149
     max_time: Optional[float] = None  # default: floor(log2(cells) + 4), src/clap_app.rs:151
     max_iter: int = MAX_ITER
@@ -171,6 +172,14 @@ class RunSpec:
     stats_target: Optional[Sequence[int]] = None  # target histogram [hist_bins] for ABC distances
     bin_kmax: int = 0  # FLAG_BIN_STORE: binned copy numbers 1..bin_kmax (0 = 64)
     _keep: list = field(default_factory=list, repr=False)
+
+    def replicate_ids(self) -> np.ndarray:
+        """Global ids of the call's replicates, in summary order."""
+        return self.first_replicate + np.arange(self.n_replicates, dtype=np.uint64) * np.uint64(
+            max(1, self.replicate_stride))
+
+    def last_replicate(self) -> int:
+        return self.first_replicate + max(0, self.n_replicates - 1) * max(1, self.replicate_stride)
 
     def resolved_max_time(self) -> float:
         if self.max_time is not None:
@@ -205,11 +214,12 @@ class RunSpec:
         p.hist_bins = self.hist_bins
         rps = self.reps_per_set
         if rps is None:
-            rps = max(1, self.first_replicate + self.n_replicates)
+            rps = max(1, self.last_replicate() + 1)
         p.reps_per_set = rps
         p.seed = self.seed
         p.first_replicate = self.first_replicate
         p.n_replicates = self.n_replicates
+        p.replicate_stride = self.replicate_stride
         p.max_cells = self.max_cells
         p.max_time = self.resolved_max_time()
         p.max_iter = self.max_iter

@@ -21,6 +21,17 @@ def shard_range(rank: int, world: int, total: int) -> Tuple[int, int]:
     return first, last - first
 
 
+def interleaved_range(rank: int, world: int, total: int) -> Tuple[int, int, int]:
+    """Strong scaling, interleaved: `rank` runs global ids rank, rank + world, rank + 2 world, ... < total,
+    as (first, n, stride) for RunSpec(first_replicate, n_replicates, replicate_stride). Every rank gets
+    the same mix of parameter sets, so an ABC sweep whose sets differ in cost (C4: initial copy numbers
+    1 .. 128) is balanced across GPUs; contiguous shards would hand each GPU one cost class."""
+    if not (0 <= rank < world):
+        raise ValueError("rank out of range")
+    n = (total - rank + world - 1) // world if total > rank else 0
+    return rank, n, world
+
+
 def weak_range(rank: int, per_rank: int) -> Tuple[int, int]:
     """Weak scaling: every rank runs `per_rank` replicates; rank g owns [g*per_rank, (g+1)*per_rank)."""
     return rank * per_rank, per_rank

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ECDNA_SSA_ABI_VERSION 4
+#define ECDNA_SSA_ABI_VERSION 5
 
 /* Process type — ProcessType (src/clap_app.rs:311-315); chosen as BirthDeath
  * when d0 > 0 or d1 > 0 (src/clap_app.rs:163-174, 194-200). */
@@ -121,9 +121,13 @@ typedef struct {
     float b0, b1, d0, d1;
 } ecdna_rates_t;
 
-/* One run = n_replicates independent replicates with global ids
- * first_replicate .. first_replicate + n_replicates - 1.
- * Replicate r uses parameter set s = r / reps_per_set (must be < n_param_sets). */
+/* One run = n_replicates independent replicates; replicate i of the call (i = 0 .. n_replicates - 1)
+ * has global id r = first_replicate + i * replicate_stride (stride 0 or 1: the contiguous ids
+ * first_replicate .. first_replicate + n_replicates - 1). Replicate r uses parameter set
+ * s = r / reps_per_set (must be < n_param_sets). Every draw is keyed by r, so a replicate's results do
+ * not depend on which call, device or position runs it: G calls with first_replicate = g and
+ * replicate_stride = G (g = 0 .. G-1) together run the same replicates as one call, interleaved so
+ * that every call gets the same mix of parameter sets (balanced ABC sweeps across GPUs). */
 typedef struct {
     int32_t process;                /* ecdna_process_t */
     int32_t segregation;            /* ecdna_seg_t */
@@ -159,7 +163,7 @@ typedef struct {
      * reference's pop_front-on-any-match rule). NULL / 0 = none. */
     const uint64_t* snapshot_cells; /* host */
     uint32_t n_snapshots;
-    uint32_t reserved2;
+    uint32_t replicate_stride;      /* global-id step between consecutive replicates of the call (0 = 1) */
     /* Per-replicate ABC summary statistics (abc.md:38-55; ECDNA_FLAG_REP_STATS): compared against this
      * target copy-number histogram of hist_bins entries (bin 0 = N- cells, last bin = overflow), e.g.
      * the patient's data. NULL: statistics are computed, distances to the target are not. */
@@ -222,7 +226,7 @@ const char* ecdna_ssa_last_error_message(void);
 int ecdna_ssa_device_count(void);
 
 /* One-shot: runs every replicate of *p on device p->device and copies the results to HOST buffers
- * (each may be NULL): out_summaries[n_replicates] (replicate first_replicate + i at index i),
+ * (each may be NULL): out_summaries[n_replicates] (replicate first_replicate + i * stride at index i),
  * out_hist[n_param_sets * hist_bins] (zeroed, then filled), out_totals[n_param_sets].
  * stream: a hipStream_t, or NULL for the default (null) stream. Blocks until done. */
 int ecdna_ssa_run(const ecdna_ssa_params_t* p, ecdna_rep_summary_t* out_summaries,

@@ -641,7 +641,7 @@ static void* worker(void* arg) {
     for (;;) {
         uint64_t i = atomic_fetch_add(&c->next, 1);
         if (i >= p->n_replicates) break;
-        uint64_t rid = p->first_replicate + i;
+        uint64_t rid = p->first_replicate + i * (p->replicate_stride ? p->replicate_stride : 1u);
         uint16_t* row = c->rows ? c->rows + i * c->row_stride : scratch;
         ecdna_rep_summary_t s;
         /* snapshot outputs: meta [n][S], rows [n][S][cell_cap] */
@@ -683,7 +683,8 @@ static int validate(const ecdna_ssa_params_t* p, uint64_t row_stride, int want_r
     if (p->process != ECDNA_PURE_BIRTH && p->process != ECDNA_BIRTH_DEATH) return ECDNA_E_INVALID;
     if (p->segregation < 0 || p->segregation > 3) return ECDNA_E_INVALID;
     if (p->max_iter > 0xffffffffull) return ECDNA_E_INVALID;
-    if (p->n_replicates && (p->first_replicate + p->n_replicates - 1) / p->reps_per_set >= p->n_param_sets)
+    const uint64_t stride = p->replicate_stride ? p->replicate_stride : 1u;
+    if (p->n_replicates && (p->first_replicate + (p->n_replicates - 1) * stride) / p->reps_per_set >= p->n_param_sets)
         return ECDNA_E_INVALID;
     if (!p->init_copies && (p->init_nplus || p->init_set_offsets)) return ECDNA_E_INVALID;
     uint64_t maxn = 0;

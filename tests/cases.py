@@ -2,7 +2,7 @@
 
 Each case is a small RunSpec the CPU oracle finishes in well under a second. Together they cover
 both processes, all four segregation rules, f32/f64 time, the birth-death cap-compat flag, single-
-and multi-set (ABC) runs, non-default initial distributions, replicate-id offsets (sharding) and
+and multi-set (ABC) runs, non-default initial distributions, replicate-id offsets and strides (sharding) and
 every stop reason and per-replicate error the engine reports.
 
 bin_cases() runs the same cases through the bin store (ECDNA_FLAG_BIN_STORE), plus
@@ -54,6 +54,11 @@ def cases():
     # replicate-id offset: a shard of a bigger run
     c["shard_offset"] = abi.RunSpec(seed=42, first_replicate=1000, n_replicates=40, max_cells=700,
                                     reps_per_set=100000, flags=H)
+    # interleaved shards (replicate_stride): ids 3, 8, ..., 198 of one set; ids 1, 4, ..., 31 across the 4 ABC sets
+    c["shard_interleaved"] = abi.RunSpec(seed=42, first_replicate=3, replicate_stride=5, n_replicates=40,
+                                         max_cells=700, reps_per_set=100000, flags=H)
+    c["abc_sets_interleaved"] = dataclasses.replace(c["abc_sets"], first_replicate=1, replicate_stride=3,
+                                                    n_replicates=11, _keep=[])
     # large copy numbers: n = 2k > 32 takes the multi-block popcount path
     c["big_copies"] = abi.RunSpec(seed=21, n_replicates=24, max_cells=300, init={40: 2, 300: 1, 5000: 1},
                                   hist_bins=64, flags=H)

@@ -14,11 +14,11 @@ import torch.multiprocessing as mp
 from ecdna_evo_amd import abi, shard
 
 
-def _spec(first, n, total):
+def _spec(first, n, total, stride=1):
     return abi.RunSpec(seed=42, process=abi.BIRTH_DEATH, segregation=abi.SEG_BINOMIAL,
                        rates=((1.0, 1.0, 0.1, 0.1), (1.0, 1.5, 0.3, 0.3), (1.0, 2.0, 0.5, 0.2)),
-                       reps_per_set=total // 3, first_replicate=first, n_replicates=n, max_cells=500,
-                       hist_bins=129, flags=abi.FLAG_EVENT_HASH)
+                       reps_per_set=total // 3, first_replicate=first, n_replicates=n, replicate_stride=stride,
+                       max_cells=500, hist_bins=129, flags=abi.FLAG_EVENT_HASH)
 
 
 def _free_port():
@@ -39,11 +39,14 @@ def _worker(rank, world, total, port, outdir, mode):
     import oracle
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    stride = 1
     if mode == "strong":
         first, n = shard.shard_range(rank, world, total)
+    elif mode == "interleaved":
+        first, n, stride = shard.interleaved_range(rank, world, total)
     else:
         first, n = shard.weak_range(rank, total // world)
-    r = oracle.run(_spec(first, n, total), mode="philox", n_threads=2)
+    r = oracle.run(_spec(first, n, total, stride), mode="philox", n_threads=2)
     hist = torch.from_numpy(r.hist.astype(np.int64).reshape(-1).copy())
     tot = torch.from_numpy(r.totals.view(np.uint64).astype(np.int64).reshape(-1).copy())
     shard.reduce_outputs(hist, tot)
@@ -55,16 +58,46 @@ def _worker(rank, world, total, port, outdir, mode):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["strong", "weak"])
+@pytest.mark.parametrize("mode", ["strong", "weak", "interleaved"])
 def test_two_rank_shards_reduce_to_single_run(oracle_mod, tmp_path, mode):
     world, total = 2, 600
     mp.spawn(_worker, args=(world, total, _free_port(), str(tmp_path), mode), nprocs=world, join=True)
     full = oracle_mod.run(_spec(0, total, total), mode="philox")
     np.testing.assert_array_equal(np.load(tmp_path / "hist.npy"), full.hist.astype(np.int64).reshape(-1))
     np.testing.assert_array_equal(np.load(tmp_path / "tot.npy"), full.totals.view(np.uint64).astype(np.int64).reshape(-1))
-    summ = np.concatenate([np.load(tmp_path / f"summ{r}.npy") for r in range(world)])
+    parts = [np.load(tmp_path / f"summ{r}.npy") for r in range(world)]
+    if mode == "interleaved":  # rank r's replicate i is global id r + i * world
+        summ = np.empty_like(full.summaries)
+        for r, part in enumerate(parts):
+            summ[r::world] = part
+    else:
+        summ = np.concatenate(parts)
     for f in full.summaries.dtype.names:
         np.testing.assert_array_equal(summ[f], full.summaries[f])
+
+
+def test_interleaved_calls_equal_one_call_per_set(oracle_mod):
+    """G interleaved calls (first_replicate = g, replicate_stride = G) run exactly the replicates of one
+    contiguous call: per-replicate results by global id, per-set histograms and totals sum to it."""
+    total, world = 96, 5
+    full = oracle_mod.run(_spec(0, total, total), mode="philox")
+    hist = np.zeros_like(full.hist.astype(np.int64))
+    for g in range(world):
+        first, n, stride = shard.interleaved_range(g, world, total)
+        assert n == len(range(g, total, world))
+        r = oracle_mod.run(_spec(first, n, total, stride), mode="philox")
+        for f in full.summaries.dtype.names:
+            np.testing.assert_array_equal(r.summaries[f], full.summaries[f][g::world])
+        hist += r.hist.astype(np.int64)
+    np.testing.assert_array_equal(hist, full.hist.astype(np.int64))
+
+
+def test_interleaved_ranges_partition():
+    for total in (1, 7, 1000, 2**20 + 3):
+        for world in (1, 2, 3, 8):
+            ids = np.sort(np.concatenate([abi.RunSpec(first_replicate=f, n_replicates=n, replicate_stride=s).replicate_ids()
+                                          for f, n, s in (shard.interleaved_range(r, world, total) for r in range(world))]))
+            np.testing.assert_array_equal(ids, np.arange(total, dtype=np.uint64))
 
 
 def test_shard_ranges_partition():

@@ -11,8 +11,10 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 from ecdna_evo_amd import abi, engine  # noqa: E402
 
 
-def c4_shard(rank=0, gpus=8):
-    """ABC sweep: 1024 (b1, d, k0) sets x 4096 replicates; rank 0's 128 sets."""
+def c4_shard(rank=0, gpus=8, interleaved=None):
+    """ABC sweep: 1024 (b1, d, k0) sets x 4096 replicates; rank `rank` of `gpus`: global
+    ids rank, rank + gpus, ... (interleaved, the default: every GPU gets every set) or the contiguous
+    block of 128 sets (PROBE_SHARD=contiguous: one initial copy number per GPU, unbalanced)."""
     rates, inits = [], []
     for i in range(1024):
         s = 1.0 + 1.5 * (i % 16) / 15.0
@@ -22,8 +24,12 @@ def c4_shard(rank=0, gpus=8):
         inits.append({k0: 1})
     per = 4096
     n = 1024 * per // gpus
-    return abi.RunSpec(seed=42, process=abi.BIRTH_DEATH, rates=rates, reps_per_set=per, first_replicate=rank * n,
-                       n_replicates=n, max_cells=10_000, init_per_set=inits, hist_bins=1025, flags=0)
+    if interleaved is None:
+        interleaved = os.environ.get("PROBE_SHARD", "interleaved") == "interleaved"
+    first, stride = (rank, gpus) if interleaved else (rank * n, 1)
+    return abi.RunSpec(seed=42, process=abi.BIRTH_DEATH, rates=rates, reps_per_set=per, first_replicate=first,
+                       n_replicates=n, replicate_stride=stride, max_cells=10_000, init_per_set=inits,
+                       hist_bins=1025, flags=0)
 
 
 def c5_shard(rank=0, gpus=8):
@@ -44,7 +50,7 @@ CONFIGS = {
 
 def main():
     for name in sys.argv[1:] or list(CONFIGS):
-        spec = CONFIGS[name]()
+        spec = CONFIGS[name](int(os.environ.get("PROBE_RANK", "0"))) if name in ("c4", "c5") else CONFIGS[name]()
         spec = dataclasses.replace(spec, flags=spec.flags | int(os.environ.get("PROBE_FLAGS", "0"), 0),
                                    bin_kmax=int(os.environ.get("PROBE_KMAX", "0")), _keep=[])
         t0 = time.time()
