@@ -202,6 +202,29 @@ def test_c4_shard_full_size_properties(engine_mod, oracle_mod, store):
 
 
 @pytest.mark.gpu
+def test_c4_interleaved_shard_full_size(engine_mod, oracle_mod):
+    """C4 rank-3 shard of 8, interleaved (global ids 3, 11, 19, ...; the layout that balances the ABC
+    grid across GPUs): every one of the 1024 sets gets 512 replicates, invariants hold,
+    and 64 replicates of set 1000 (initial k = 128: 256-bit binomials through the block-wise popcount,
+    cells beyond the LDS bins) match the oracle bit for bit."""
+    from ecdna_evo_amd import shard
+
+    first, n, stride = shard.interleaved_range(3, 8, 1024 * 4096)
+    spec = c4_shard_spec(first_replicate=first, n_replicates=n, replicate_stride=stride,
+                         flags=abi.FLAG_EVENT_HASH | abi.FLAG_BIN_STORE, bin_kmax=32)
+    r = engine_mod.run(spec)
+    _invariants(r, spec)
+    assert np.all(r.totals["replicates"] == 512)
+    m0 = (1000 * 4096 - first + stride - 1) // stride  # first local replicate in set 1000
+    sub = c4_shard_spec(first_replicate=first + m0 * stride, n_replicates=64, replicate_stride=stride,
+                        flags=abi.FLAG_EVENT_HASH | abi.FLAG_BIN_STORE, bin_kmax=32)
+    assert (sub.first_replicate // 4096) == 1000
+    c = oracle_mod.run(sub, mode="philox", n_threads=4)
+    for f in c.summaries.dtype.names:
+        np.testing.assert_array_equal(r.summaries[f][m0:m0 + 64], c.summaries[f], err_msg=f)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("store", sorted(STORES))
 def test_c5_shard_full_size_properties(engine_mod, oracle_mod, store):
     """C5 rank-0 shard at full size (32,768 replicates, rows up to 1e6 cells = 2 MB, 65 GB of rows):
