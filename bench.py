@@ -15,6 +15,13 @@ Cell store (--store): "bins" (default, ECDNA_FLAG_BIN_STORE: per-replicate copy-
 LDS) or "rows" (one u16 per cell in HBM in the reference's swap_remove order). Both
 simulate the same process and count the same events; each is bit-exact with its oracle restatement.
 
+Other BASELINE.json configs (--workload; the default line above is C3): c2 = 65,536 pure-birth replicates
+to 1e4 cells (configs[1]); c4 = the ABC sweep, 1024 (b1, d, k0) parameter sets x 4,096 replicates
+(configs[3]); c5 = 262,144 birth-death turnover replicates from 1,000 cells to 1e6 cells or t = 1000
+(configs[4]). These are strong-scaling runs of a fixed total, sharded over the ranks by interleaved
+global ids (rank g of G runs ids g, g+G, ...: every GPU gets the same mix of parameter sets,
+DESIGN.md §7).
+
 Extra JSON fields:
   roofline      — the stepper kernel against HBM: algorithmic bytes per launch over
                   its average duration (HIP events on the launch stream), vs 8 TB/s; `traffic` =
@@ -77,11 +84,42 @@ BENCH_BIN_KMAX = 32
 
 
 def workload_spec(first: int, n: int, total: int, seed: int = 42, device: int = 0, store: str = "bins",
-                  bin_kmax: int = BENCH_BIN_KMAX) -> abi.RunSpec:
-    return abi.RunSpec(process=abi.BIRTH_DEATH, segregation=abi.SEG_BINOMIAL, rates=((1.0, 1.5, 0.3, 0.3),),
-                       reps_per_set=total, seed=seed, first_replicate=first, n_replicates=n, max_cells=10_000,
-                       hist_bins=1025, flags=abi.FLAG_BIN_STORE if store == "bins" else 0,
-                       bin_kmax=bin_kmax if store == "bins" else 0, device=device)
+                  bin_kmax: int = BENCH_BIN_KMAX, workload: str = "c3", stride: int = 1) -> abi.RunSpec:
+    """Replicates first, first + stride, ... (n of them) of the workload's `total` (SURVEY.md §8d shapes)."""
+    common = dict(seed=seed, first_replicate=first, n_replicates=n, replicate_stride=stride, hist_bins=1025,
+                  flags=abi.FLAG_BIN_STORE if store == "bins" else 0, device=device)
+    if workload == "c3":
+        d = dict(process=abi.BIRTH_DEATH, rates=((1.0, 1.5, 0.3, 0.3),), reps_per_set=total, max_cells=10_000)
+    elif workload == "c2":
+        d = dict(process=abi.PURE_BIRTH, rates=((1.0, 1.0, 0.0, 0.0),), reps_per_set=total, max_cells=10_000)
+    elif workload == "c4":  # b1 = b0 * s (16 values in [1, 2.5]), d0 = d1 = d (8 values in [0, 0.7]), k0 = 1 .. 128
+        rates, inits = [], []
+        for i in range(1024):
+            sel, dd = 1.0 + 1.5 * (i % 16) / 15.0, 0.7 * ((i // 16) % 8) / 7.0
+            rates.append((1.0, sel, dd, dd))
+            inits.append({1 << (i // 128): 1})
+        d = dict(process=abi.BIRTH_DEATH, rates=rates, reps_per_set=total // 1024, max_cells=10_000,
+                 init_per_set=inits)
+    elif workload == "c5":
+        d = dict(process=abi.BIRTH_DEATH, rates=((1.0, 1.0, 0.9, 0.9),), reps_per_set=total, max_cells=1_000_000,
+                 max_time=1000.0, init={1: 1000})
+        bin_kmax = 64  # broad copy numbers at 1e6 cells (DESIGN.md §8)
+    else:
+        raise ValueError(workload)
+    return abi.RunSpec(segregation=abi.SEG_BINOMIAL, bin_kmax=bin_kmax if store == "bins" else 0, **common, **d)
+
+
+# --workload: (replicates: per GPU for the weak-scaling C3 line, total otherwise; description)
+WORKLOADS = {
+    "c3": (REPS_PER_GPU, "C3 (BASELINE.json configs[2]): 2^20 replicates/GPU, birth-death b0=1 b1=1.5 d0=d1=0.3, "
+                         "binomial segregation, init {1:1}, stop 1e4 cells or t=17, seed 42"),
+    "c2": (65_536, "C2 (BASELINE.json configs[1]): 65,536 replicates in total, pure birth b=1, binomial "
+                   "segregation, init {1:1}, stop 1e4 cells or t=17, seed 42"),
+    "c4": (4_194_304, "C4 (BASELINE.json configs[3]): ABC sweep, 1024 (b1, d, k0) sets x 4,096 replicates = "
+                      "4,194,304 in total, stop 1e4 cells or t=17, seed 42"),
+    "c5": (262_144, "C5 (BASELINE.json configs[4]): 262,144 replicates in total, birth-death turnover b=1 d=0.9, "
+                    "binomial segregation, init {1:1000}, stop 1e6 cells or t=1000, seed 42"),
+}
 
 
 def algorithmic_bytes(words, n_reps: int, init_cells: int = 1) -> int:
@@ -116,30 +154,33 @@ def rmw_ceiling():
     return best
 
 
-def cpu_baseline(threads: int):
-    """Reference-semantics CPU path (oracle compat mode) timed on a bounded sample of the workload."""
+def cpu_baseline(threads: int, workload: str = "c3"):
+    """Reference-semantics CPU path (oracle compat mode) timed on a bounded sample of the workload: its
+    first replicates (C4: ids spread evenly over the id range, so the sample spans every set)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # test infrastructure: the CPU baseline only
 
-    t0 = time.time()
-    probe = workload_spec(0, 1024, REPS_PER_GPU)
-    r = oracle.run(probe, mode="compat", n_threads=threads)
-    dt = max(time.time() - t0, 1e-3)
+    total = WORKLOADS[workload][0]
+
+    def sample(n, mode):
+        stride = max(1, total // n) if workload == "c4" else 1  # C4: evenly spread over the 1024 sets
+        spec = workload_spec(0, n, total, workload=workload, stride=stride)
+        t0 = time.time()
+        r = oracle.run(spec, mode=mode, n_threads=threads)
+        return int(r.totals["events"].sum()), max(time.time() - t0, 1e-3)
+
+    n0 = 16 if workload == "c5" else 1024  # C5: ~2e7 events per replicate
+    _, dt = sample(n0, "compat")
     target_s = float(os.environ.get("ECDNA_BENCH_CPU_SECONDS", "10"))
-    n = int(min(REPS_PER_GPU, max(1024, 1024 * target_s / dt)))
-    spec = workload_spec(0, n, REPS_PER_GPU)
-    t0 = time.time()
-    r = oracle.run(spec, mode="compat", n_threads=threads)
-    dt = time.time() - t0
-    ev = int(r.totals["events"].sum())
+    n = int(min(total, max(n0, n0 * target_s / dt)))
+    ev, dt = sample(n, "compat")
     # for information (SURVEY.md §8d): the same sample through the engine's own draw mapping on the CPU
-    n_ph = max(1024, n // 2)
-    t0 = time.time()
-    rp = oracle.run(workload_spec(0, n_ph, REPS_PER_GPU), mode="philox", n_threads=threads)
-    dt_ph = time.time() - t0
-    ev_ph = int(rp.totals["events"].sum())
+    n_ph = max(n0, n // 2)
+    ev_ph, dt_ph = sample(n_ph, "philox")
+    what = "C3 shape, replicates 0..{0} of 2^20".format(n - 1) if workload == "c3" else \
+        f"{workload.upper()} shape, {n} of its {total} replicates"
     return {"value": ev / dt, "unit": "events/s", "cores": threads, "kind": "port",
-            "sample": f"C3 shape, replicates 0..{n - 1} of 2^20 ({ev} events, {dt:.1f} s wall), "
+            "sample": f"{what} ({ev} events, {dt:.1f} s wall), "
                       f"oracle compat mode (ChaCha8 streams seed*10+i, first-reaction, BTPE), "
                       f"{threads} threads",
             "philox_mode_value": ev_ph / dt_ph,
@@ -162,6 +203,8 @@ def main():
     ap.add_argument("--store", choices=("bins", "rows"), default="bins")
     ap.add_argument("--bin-kmax", type=int, choices=(32, 64, 256), default=BENCH_BIN_KMAX)
     ap.add_argument("--dump-hist", default="", help="rank 0 saves the reduced histogram and totals (.npz)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3",
+                    help="BASELINE.json config; c3 (default) is the metric's weak-scaling line")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -183,15 +226,22 @@ def main():
     else:
         torch.cuda.set_device(0)
     n_gpus = world
-    reps = args.reps_per_gpu
-    total = reps * n_gpus
-
-    first, n = shard.weak_range(rank, reps)
+    weak = args.workload == "c3"
+    if weak:  # the metric's line: 2^20 replicates per GPU, rank g owns ids [g 2^20, (g+1) 2^20)
+        reps = args.reps_per_gpu
+        total = reps * n_gpus
+        first, n = shard.weak_range(rank, reps)
+        stride = 1
+    else:  # a fixed total over the ranks, interleaved ids
+        total = WORKLOADS[args.workload][0]
+        first, n, stride = shard.interleaved_range(rank, n_gpus, total)
+        reps = n
     spec = workload_spec(first, n, total, device=local if distributed else 0, store=args.store,
-                         bin_kmax=args.bin_kmax)
+                         bin_kmax=args.bin_kmax, workload=args.workload, stride=stride)
+    n_sets = len(spec.rates)
     ctx = engine.Context(spec)
-    hist = torch.zeros(spec.hist_bins, dtype=torch.int64, device="cuda")
-    tot = torch.zeros(16, dtype=torch.int64, device="cuda")
+    hist = torch.zeros(n_sets * spec.hist_bins, dtype=torch.int64, device="cuda")
+    tot = torch.zeros(n_sets * 16, dtype=torch.int64, device="cuda")
     ctx.set_outputs(hist.data_ptr(), tot.data_ptr())
     torch_stream = torch.cuda.Stream()
     torch.cuda.set_stream(torch_stream)  # torch ops and the engine's kernels share this stream
@@ -225,9 +275,9 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
 
-    local_words = tot_local.cpu().numpy()
+    local_words = tot_local.cpu().numpy().reshape(n_sets, 16).sum(axis=0)  # per-set totals, summed
     local_events = int(local_words[1])
-    local_alg = algorithmic_bytes(local_words, reps)
+    local_alg = algorithmic_bytes(local_words, reps, init_cells=1000 if args.workload == "c5" else 1)
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     ev = torch.tensor([local_events], dtype=torch.int64, device="cuda")
     if distributed:
@@ -236,14 +286,15 @@ def main():
     elapsed = float(t.item())
     events_per_step = int(ev.item())
     # the all-reduced histogram must account for every cell of every replicate
-    tot_host = tot.cpu().numpy()
+    tot_sets = tot.cpu().numpy()
+    tot_host = tot_sets.reshape(n_sets, 16).sum(axis=0)
     assert int(tot_host[0]) == total, f"all-reduced totals count {int(tot_host[0])} replicates, expected {total}"
     assert int(tot_host[1]) == events_per_step
 
     if rank == 0 and args.dump_hist:
         import numpy as np
 
-        np.savez(args.dump_hist, hist=hist.cpu().numpy(), totals=tot_host)
+        np.savez(args.dump_hist, hist=hist.cpu().numpy(), totals=tot_sets)
     if rank == 0:
         avg_kernel_s = sum(kernel_ms) / len(kernel_ms) * 1e-3
         achieved = local_alg / avg_kernel_s / 1e9
@@ -252,7 +303,7 @@ def main():
         kernel_eps = local_events / avg_kernel_s
         transactions = None
         issue = None
-        if args.store == "bins" and "valu_insts_per_event" in pmc:
+        if args.store == "bins" and weak and "valu_insts_per_event" in pmc:  # (the PMC summary is C3's)
             per_event = pmc["valu_insts_per_event"]
             two, four = valu_measured_ceilings()
             issue = {
@@ -269,7 +320,7 @@ def main():
                         "wave64 instruction, which only the VOP2 logic/add/mov class reaches on gfx950 — most of "
                         "the stepper's instructions are in the measured 4-cycle class (tools/valu_probe.hip)",
             }
-        if args.store == "rows" and "read_requests_per_event" in pmc:
+        if args.store == "rows" and weak and "read_requests_per_event" in pmc:
             per_event = pmc["read_requests_per_event"] + pmc["write_requests_per_event"]
             ceiling = rmw_ceiling()
             transactions = {
@@ -284,10 +335,10 @@ def main():
         cpu = None
         if n_gpus == 1 and not args.no_cpu_baseline:
             threads = int(os.environ.get("ECDNA_BENCH_CPU_THREADS", "0")) or min(16, os.cpu_count() or 1)
-            cpu = cpu_baseline(threads)
+            cpu = cpu_baseline(threads, args.workload)
         chunk, lanes = ctx.geometry()
         line = {
-            "metric": METRIC,
+            "metric": METRIC if weak else f"Gillespie reaction-events/sec, {args.workload.upper()}",
             "value": events_per_step * args.steps / elapsed,
             "unit": "events/s",
             "n_gpus": n_gpus,
@@ -295,20 +346,20 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if weak else "strong",
             "vs_baseline": None,
             "dtype": "u16+f64",
             "store": args.store,
             "data": "synthetic",
             "config": {
-                "workload": "C3 (BASELINE.json configs[2]): 2^20 replicates/GPU, birth-death b0=1 b1=1.5 "
-                            "d0=d1=0.3, binomial segregation, init {1:1}, stop 1e4 cells or t=17, seed 42",
-                "cell_store": f"bins (copy-number counters in LDS, k<={args.bin_kmax}; ECDNA_FLAG_BIN_STORE)"
+                "workload": WORKLOADS[args.workload][1],
+                "cell_store": f"bins (copy-number counters in LDS, k<={spec.bin_kmax}; ECDNA_FLAG_BIN_STORE)"
                               if args.store == "bins" else "rows (u16 per cell in HBM, swap_remove order)",
                 "replicates_per_gpu": reps,
                 "replicates_total": total,
                 "events_per_step": events_per_step,
-                "parallelism": f"replicas{n_gpus} (replicate-id shards, 1 RCCL all-reduce of the histogram)",
+                "parallelism": f"replicas{n_gpus} ({'contiguous' if weak else 'interleaved'} replicate-id shards, "
+                               f"1 RCCL all-reduce of the histogram)",
                 "grid_lanes": lanes,
                 "kernel_ms_avg": avg_kernel_s * 1e3,
                 "hist_kernel_ms_avg": sum(hist_ms) / len(hist_ms),

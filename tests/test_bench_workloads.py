@@ -1,0 +1,55 @@
+"""bench.py's workloads (BASELINE.json configs C2-C5) on the CPU: every rank's shard is a valid run of
+the engine's ABI, the shards of a strong-scaling workload partition its total, C4's interleaved shards
+give every rank every parameter set, and a few replicates of each workload run through the oracle with
+the bookkeeping identities of the reference's events (tests/test_gpu_statistics.py runs them at full
+size on the GPU)."""
+import numpy as np
+import pytest
+
+import bench
+from ecdna_evo_amd import abi, shard
+
+
+@pytest.mark.parametrize("workload", sorted(bench.WORKLOADS))
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_workload_shards_partition_the_total(workload, world):
+    total = bench.WORKLOADS[workload][0]
+    if workload == "c3":
+        total *= world  # weak scaling: 2^20 per rank
+    ids = []
+    for rank in range(world):
+        if workload == "c3":
+            first, n = shard.weak_range(rank, total // world)
+            stride = 1
+        else:
+            first, n, stride = shard.interleaved_range(rank, world, total)
+        spec = bench.workload_spec(first, n, total, workload=workload, stride=stride)
+        p = spec.params()
+        assert p.n_replicates == n and (p.replicate_stride or 1) == stride
+        last = spec.last_replicate()
+        assert last // p.reps_per_set < p.n_param_sets
+        if workload == "c4":  # interleaved: every rank holds all 1024 sets, 4096 / world replicates each
+            sets = np.bincount((spec.replicate_ids() // p.reps_per_set).astype(np.int64), minlength=1024)
+            assert np.all(sets == 4096 // world)
+        ids.append(spec.replicate_ids())
+    ids = np.sort(np.concatenate(ids))
+    np.testing.assert_array_equal(ids, np.arange(total, dtype=np.uint64))
+
+
+@pytest.mark.parametrize("workload", sorted(bench.WORKLOADS))
+def test_workload_sample_runs_on_the_oracle(oracle_mod, workload):
+    total = bench.WORKLOADS[workload][0]
+    n = 1 if workload == "c5" else 24
+    stride = total // n if workload == "c4" else 1
+    spec = bench.workload_spec(0, n, total, workload=workload, stride=stride)
+    r = oracle_mod.run(spec, mode="philox", n_threads=4)
+    s = r.summaries
+    assert np.all(s["error"] == 0)
+    ev = s["events_by_type"].astype(np.int64)
+    np.testing.assert_array_equal(ev.sum(axis=1), s["iters"].astype(np.int64))
+    assert int(r.totals["replicates"].sum()) == n
+    if workload == "c2":  # pure birth: exactly max_cells - 1 events from one cell (or the time cap)
+        full = s["stop_reason"] == abi.STOP_MAX_CELLS
+        assert np.all(s["iters"][full] == 10_000 - 1)
+    if workload == "c5":  # 1,000 initial cells; the run ends at 1e6 cells or extinction
+        assert s["stop_reason"][0] in (abi.STOP_MAX_CELLS, abi.STOP_ABSORBING)
