@@ -99,7 +99,7 @@ def workload_spec(first: int, n: int, total: int, seed: int = 42, device: int = 
             rates.append((1.0, sel, dd, dd))
             inits.append({1 << (i // 128): 1})
         d = dict(process=abi.BIRTH_DEATH, rates=rates, reps_per_set=total // 1024, max_cells=10_000,
-                 init_per_set=inits)
+                 init_per_set=inits, set_cost_hint=abi.cost_hint(rates, inits))  # costly sets start first
     elif workload == "c5":
         d = dict(process=abi.BIRTH_DEATH, rates=((1.0, 1.0, 0.9, 0.9),), reps_per_set=total, max_cells=1_000_000,
                  max_time=1000.0, init={1: 1000})

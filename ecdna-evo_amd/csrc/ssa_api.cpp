@@ -145,6 +145,7 @@ struct ecdna_ssa_ctx {
     uint16_t* d_rows = nullptr;
     ecdna_rep_summary_t* d_summ = nullptr;
     uint32_t* d_heads = nullptr;  // one work counter per chunk
+    uint32_t* d_order = nullptr;  // [n] chunk-local start order (set_cost_hint) or nullptr
     // replicate rotation (bin store): per-partition counters, state bytes, parked scalars (one chunk's worth)
     ecdna::RotPart* d_rot_parts = nullptr;
     uint32_t* d_rot_flags = nullptr;
@@ -199,6 +200,7 @@ void free_ctx(ecdna_ssa_ctx* c) {
     (void)hipFree(c->d_bags);
     (void)hipFree(c->d_summ);
     (void)hipFree(c->d_heads);
+    (void)hipFree(c->d_order);
     (void)hipFree(c->d_rot_parts);
     (void)hipFree(c->d_rot_flags);
     (void)hipFree(c->d_rot_park);
@@ -388,6 +390,23 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
         for (auto& e : c->chunks.back().ev) CTX_TRY(hipEventCreate(&e));
     }
 
+    // start order (set_cost_hint): within each chunk, replicates of costlier sets first, then by id
+    if (p->set_cost_hint && n) {
+        const uint64_t stride = p->replicate_stride ? p->replicate_stride : 1u;
+        std::vector<uint32_t> order(n);
+        for (const Chunk& ch : c->chunks) {
+            uint32_t* o = order.data() + ch.first;
+            for (uint32_t i = 0; i < ch.n; ++i) o[i] = i;
+            auto cost = [&](uint32_t i) {
+                const float v = p->set_cost_hint[(p->first_replicate + (ch.first + i) * stride) / p->reps_per_set];
+                return v == v ? v : 0.0f;  // (NaN: no preference)
+            };
+            std::stable_sort(o, o + ch.n, [&](uint32_t x, uint32_t y) { return cost(x) > cost(y); });
+        }
+        CTX_TRY(hipMalloc(&c->d_order, n * sizeof(uint32_t)));
+        CTX_TRY(hipMemcpy(c->d_order, order.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
+
     // persistent stepper grid: as many resident lanes as the occupancy allows
     c->window = env_u64("ECDNA_SSA_WINDOW", 1) ? 1 : 0;
     int per_cu = 0;
@@ -476,6 +495,7 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
         a.rows = c->d_rows;
         a.summaries = c->d_summ + ch.first;
         a.head = c->d_heads + k;
+        a.order = c->d_order ? c->d_order + ch.first : nullptr;
         a.rates = c->d_rates;
         a.init_copies = c->d_init;
         a.init_offsets = c->d_init_off;

@@ -141,8 +141,9 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
                 s->stop_reason = stop;
                 s->error = err;
             }
-            const uint32_t i = atomicAdd(a.head, 1u);
+            uint32_t i = atomicAdd(a.head, 1u);
             if (i >= a.n) break;
+            if (a.order) i = a.order[i];
             have = true;
             active = true;
             li = i;
@@ -485,7 +486,11 @@ __device__ __forceinline__ uint32_t rot_claim(KArgs* ra, uint32_t pp, bool fresh
         if (fresh_only && j >= n_pad) return 0u;  // past the first pass: no fresh replicate is left
         // partitions interleave the replicates (r mod kRotParts), so a run whose cost varies along the
         // replicate order (an ABC sweep's parameter sets) gives every XCD the same mix
-        const uint32_t r = pp + kRotParts * (j < (1ull << 32) ? (uint32_t)j % n_pad : (uint32_t)(j % n_pad));
+        uint32_t r = pp + kRotParts * (j < (1ull << 32) ? (uint32_t)j % n_pad : (uint32_t)(j % n_pad));
+        if (ra->order) {  // item r starts the order's r-th replicate (costliest sets first); past n: padding
+            if (r >= ra->n) continue;
+            r = ra->order[r];
+        }
         // blind compare-and-swap from the likelier waiting state; the value it returns says whether the
         // item is FRESH after all (one more try) or not waiting (RUNNING / DONE: next item)
         uint32_t st = fresh_only ? (uint32_t)ROT_FRESH : (uint32_t)ROT_PARKED;
@@ -768,6 +773,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                     break;
                 i = atomicAdd(ra->head, 1u);
                 if (i >= ra->n) break;
+                if (ra->order) i = ra->order[i];
             }
             have = true;
             active = true;

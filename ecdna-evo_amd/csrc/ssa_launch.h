@@ -30,6 +30,7 @@ struct StepperArgs {
     uint16_t* rows;                 // [n][row_stride] per-replicate N+ rows (replicate-major)
     ecdna_rep_summary_t* summaries; // [n], already offset to the chunk
     uint32_t* head;                 // work counter (zeroed before the launch)
+    const uint32_t* order;          // [n] chunk-local start order (costliest sets first) or nullptr: id order
     const float4* rates;            // [n_param_sets] (b0, b1, d0, d1)
     const uint16_t* init_copies;
     const uint32_t* init_offsets;   // [n_sets + 1] or nullptr (shared initial distribution)

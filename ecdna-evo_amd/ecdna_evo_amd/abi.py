@@ -86,6 +86,7 @@ class Params(C.Structure):
         ("n_snapshots", C.c_uint32),
         ("replicate_stride", C.c_uint32),
         ("stats_target_hist", C.POINTER(C.c_uint64)),
+        ("set_cost_hint", C.POINTER(C.c_float)),
     ]
 
 
@@ -171,6 +172,7 @@ class RunSpec:
     snapshots: Optional[Sequence[int]] = None  # cell counts (sorted here); None = no snapshots
     stats_target: Optional[Sequence[int]] = None  # target histogram [hist_bins] for ABC distances
     bin_kmax: int = 0  # FLAG_BIN_STORE: binned copy numbers 1..bin_kmax (0 = 64)
+    set_cost_hint: Optional[Sequence[float]] = None  # per set: start costlier sets first (speed only)
     _keep: list = field(default_factory=list, repr=False)
 
     def replicate_ids(self) -> np.ndarray:
@@ -231,6 +233,12 @@ class RunSpec:
             self._keep.append(snaps)
             p.snapshot_cells = _ptr(snaps, C.c_uint64)
             p.n_snapshots = len(snaps)
+        if self.set_cost_hint is not None:
+            hint = np.asarray(self.set_cost_hint, dtype=np.float32)
+            if hint.shape != (n_sets,):
+                raise ValueError("set_cost_hint needs one value per parameter set")
+            self._keep.append(hint)
+            p.set_cost_hint = _ptr(hint, C.c_float)
         if self.stats_target is not None:
             tgt = np.asarray(self.stats_target, dtype=np.uint64)
             if tgt.shape != (self.hist_bins,):
@@ -266,6 +274,25 @@ class RunSpec:
             cap = max(int(min(self.max_cells, 2**32 - 1)), max_np, 1)
         p.cell_cap = cap
         return p
+
+
+def cost_hint(rates: Sequence[Sequence[float]], inits: Optional[Sequence[Dict[int, int]]] = None) -> List[float]:
+    """A rough relative cost per replicate of each parameter set, for RunSpec.set_cost_hint: events to grow
+    a birth-death population scale with (b1 + d1) / (b1 - d1) (net growth per event of the N+ type), and
+    an event costs more as copy numbers grow (2k segregation bits beyond the first Philox words, cells
+    beyond the LDS bins): factor 1 + mean initial copy number / 16. Only the ORDER of the values matters
+    (longest-processing-time starts); a poor estimate costs speed, never results."""
+    out = []
+    for s, r in enumerate(rates):
+        b1, d1 = float(r[1]), float(r[3])
+        events = (b1 + d1) / max(b1 - d1, 0.05)
+        k = 1.0
+        if inits is not None:
+            h = {int(key): int(v) for key, v in inits[s].items() if int(key) > 0}
+            if h:
+                k = sum(key * v for key, v in h.items()) / max(1, sum(h.values()))
+        out.append(events * (1.0 + k / 16.0))
+    return out
 
 
 def summaries_array(n: int) -> np.ndarray:

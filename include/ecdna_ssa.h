@@ -168,6 +168,11 @@ typedef struct {
      * target copy-number histogram of hist_bins entries (bin 0 = N- cells, last bin = overflow), e.g.
      * the patient's data. NULL: statistics are computed, distances to the target are not. */
     const uint64_t* stats_target_hist; /* host */
+    /* Scheduling hint (optional, host, n_param_sets entries): the relative cost of one replicate of each
+     * parameter set. Replicates of costlier sets are started first (longest-processing-time order, ties
+     * in id order), which shortens the tail of a run whose sets differ in cost, such as an ABC sweep.
+     * Results do not depend on it. NULL: replicates start in id order. */
+    const float* set_cost_hint;
 } ecdna_ssa_params_t;
 
 /* Per-replicate summary statistics of the final distribution (cells = n- + n+, copy number k per cell,

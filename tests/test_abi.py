@@ -141,3 +141,15 @@ def test_no_device_fails_loudly(product_lib):
 def test_strerror(product_lib):
     for code in (0, -1, -2, -3, -4, -5, -99):
         assert product_lib.ecdna_ssa_strerror(code)
+
+
+def test_set_cost_hint_in_params():
+    import ctypes as C
+
+    spec = abi.RunSpec(rates=((1, 1, 0, 0), (1, 2, 0, 0)), reps_per_set=4, n_replicates=8, set_cost_hint=[1.0, 3.0])
+    p = spec.params()
+    assert p.set_cost_hint[0] == 1.0 and p.set_cost_hint[1] == 3.0
+    assert not abi.RunSpec(n_replicates=4).params().set_cost_hint  # NULL by default
+    with pytest.raises(ValueError):
+        abi.RunSpec(rates=((1, 1, 0, 0),), set_cost_hint=[1.0, 2.0]).params()
+    assert C.sizeof(abi.Params) % 8 == 0

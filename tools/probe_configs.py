@@ -27,9 +27,10 @@ def c4_shard(rank=0, gpus=8, interleaved=None):
     if interleaved is None:
         interleaved = os.environ.get("PROBE_SHARD", "interleaved") == "interleaved"
     first, stride = (rank, gpus) if interleaved else (rank * n, 1)
+    hint = abi.cost_hint(rates, inits) if os.environ.get("PROBE_COST_HINT", "1") == "1" else None
     return abi.RunSpec(seed=42, process=abi.BIRTH_DEATH, rates=rates, reps_per_set=per, first_replicate=first,
                        n_replicates=n, replicate_stride=stride, max_cells=10_000, init_per_set=inits,
-                       hist_bins=1025, flags=0)
+                       hist_bins=1025, flags=0, set_cost_hint=hint)
 
 
 def c5_shard(rank=0, gpus=8):
