@@ -101,9 +101,11 @@ def workload_spec(first: int, n: int, total: int, seed: int = 42, device: int = 
         d = dict(process=abi.BIRTH_DEATH, rates=rates, reps_per_set=total // 1024, max_cells=10_000,
                  init_per_set=inits, set_cost_hint=abi.cost_hint(rates, inits))  # costly sets start first
     elif workload == "c5":
+        # broad copy numbers at 1e6 cells: K = 64; the large-k row holds at most 2^16 cells (128 KB
+        # per replicate instead of cell_cap's 2 MB, so the 262,144 replicates fit in HBM in one chunk)
         d = dict(process=abi.BIRTH_DEATH, rates=((1.0, 1.0, 0.9, 0.9),), reps_per_set=total, max_cells=1_000_000,
-                 max_time=1000.0, init={1: 1000})
-        bin_kmax = 64  # broad copy numbers at 1e6 cells
+                 max_time=1000.0, init={1: 1000}, big_cap=1 << 16 if store == "bins" else 0)
+        bin_kmax = 64
     else:
         raise ValueError(workload)
     return abi.RunSpec(segregation=abi.SEG_BINOMIAL, bin_kmax=bin_kmax if store == "bins" else 0, **common, **d)

@@ -90,6 +90,12 @@ int validate(const ecdna_ssa_params_t* p) {
     for (uint32_t s = 0; s < p->n_param_sets; ++s) {
         InitOfSet in = init_of_set(p, s);
         if (in.nplus > p->cell_cap) return fail(ECDNA_E_INVALID, "initial N+ cells exceed cell_cap");
+        if ((p->flags & ECDNA_FLAG_BIN_STORE) && p->big_cap) {
+            const uint32_t kmax = p->bin_kmax ? p->bin_kmax : 64u;
+            uint64_t big = 0;
+            for (uint64_t j = 0; j < in.nplus; ++j) big += in.copies[j] > kmax;
+            if (big > p->big_cap) return fail(ECDNA_E_INVALID, "initial cells above bin_kmax exceed big_cap");
+        }
         if (in.nminus > 0xffffffffull) return fail(ECDNA_E_INVALID, "initial N- cells must be < 2^32");
         for (uint64_t j = 0; j < in.nplus; ++j)
             if (in.copies[j] == 0) return fail(ECDNA_E_INVALID, "initial copy numbers must be >= 1");
@@ -113,7 +119,9 @@ struct ecdna_ssa_ctx {
     ecdna_ssa_params_t p{};
     int device = 0;
     int cus = 0;
-    uint64_t row_stride = 0;
+    uint64_t row_stride = 0;  // device rows (the bin store: its large-k rows, big_cap cells)
+    uint64_t out_stride = 0;  // downloaded and snapshot rows (cell_cap cells)
+    uint32_t big_cap = 0;     // bin store: large-k row capacity
     uint64_t chunk_reps = 0;
     uint32_t stepper_blocks_cap = 0;
     int window = 1;  // LDS tail window stepper (ECDNA_SSA_WINDOW=0 selects the HBM-only variant)
@@ -349,7 +357,10 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
     CTX_TRY(hipMalloc(&c->d_summ, std::max<uint64_t>(n, 1) * sizeof(ecdna_rep_summary_t)));
 
     c->row_stride = round_up(p->cell_cap, 64);
+    c->out_stride = c->row_stride;
     if (p->flags & ECDNA_FLAG_BIN_STORE) {
+        c->big_cap = (p->big_cap && p->big_cap < p->cell_cap) ? p->big_cap : p->cell_cap;
+        c->row_stride = round_up(c->big_cap, 64);
         c->bin_k = p->bin_kmax ? p->bin_kmax : 64;
         // u16 counters hold at most 65535 cells per bin/group; K = 32 always uses u32 counters: the same LDS
         // footprint as K = 64/u16 (144 B per lane), no 16-bit packing in the updates and the scan (C3:
@@ -361,7 +372,7 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
     if (p->n_snapshots && n) {  // snapshot outputs cover the whole run (not chunked)
         CTX_TRY(hipMalloc(&c->d_snap_meta, n * p->n_snapshots * sizeof(ecdna_snapshot_t)));
         if (p->flags & ECDNA_FLAG_SNAPSHOT_ROWS)
-            CTX_TRY(hipMalloc(&c->d_snap_rows, n * p->n_snapshots * c->row_stride * sizeof(uint16_t)));
+            CTX_TRY(hipMalloc(&c->d_snap_rows, n * p->n_snapshots * c->out_stride * sizeof(uint16_t)));
     }
 
     // rows: one u16 row per replicate of the chunk; chunk bounded by free HBM
@@ -522,7 +533,9 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
         a.n_snap = p.n_snapshots;
         a.snap_cells = c->d_snap_cells;
         a.snap_meta = c->d_snap_meta ? c->d_snap_meta + ch.first * p.n_snapshots : nullptr;
-        a.snap_rows = c->d_snap_rows ? c->d_snap_rows + ch.first * p.n_snapshots * c->row_stride : nullptr;
+        a.snap_rows = c->d_snap_rows ? c->d_snap_rows + ch.first * p.n_snapshots * c->out_stride : nullptr;
+        a.snap_stride = c->out_stride;
+        a.big_cap = c->big_cap;
         a.bags = c->d_bags;
         const uint32_t need = (ch.n + c->stepper_block - 1) / c->stepper_block;
         const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(need, c->stepper_blocks_cap));
@@ -623,7 +636,7 @@ int ecdna_ssa_ctx_device_outputs(ecdna_ssa_ctx* c, uint64_t** d_hist, ecdna_tota
 
 int64_t ecdna_ssa_ctx_row_stride(const ecdna_ssa_ctx* c) {
     if (!c) return 0;
-    return c->chunks.size() <= 1 ? (int64_t)c->row_stride : 0;
+    return c->chunks.size() <= 1 ? (int64_t)c->out_stride : 0;
 }
 
 int ecdna_ssa_ctx_geometry(const ecdna_ssa_ctx* c, uint64_t* chunk_replicates, uint64_t* grid_lanes) {
@@ -650,10 +663,12 @@ int ecdna_ssa_ctx_download(ecdna_ssa_ctx* c, ecdna_rep_summary_t* out_summaries,
         HIP_TRY(hipMemcpy(out_totals, c->d_tot, p.n_param_sets * sizeof(ecdna_totals_t), hipMemcpyDeviceToHost));
     if (out_rows) {
         if (c->chunks.size() > 1) return fail(ECDNA_E_STATE, "rows are not downloadable from a chunked run");
-        if (p.n_replicates)
+        if (p.n_replicates && !c->bin_k)
             HIP_TRY(hipMemcpy(out_rows, c->d_rows, p.n_replicates * c->row_stride * sizeof(uint16_t),
                               hipMemcpyDeviceToHost));
         if (c->bin_k && p.n_replicates) {
+            std::vector<uint16_t> dev_rows(p.n_replicates * c->row_stride);  // the large-k rows
+            HIP_TRY(hipMemcpy(dev_rows.data(), c->d_rows, dev_rows.size() * sizeof(uint16_t), hipMemcpyDeviceToHost));
             // bin store: canonical rows = the counters expanded (k ascending), then the large-k row
             std::vector<ecdna_rep_summary_t> summ(p.n_replicates);
             HIP_TRY(hipMemcpy(summ.data(), c->d_summ, p.n_replicates * sizeof(ecdna_rep_summary_t),
@@ -669,16 +684,17 @@ int ecdna_ssa_ctx_download(ecdna_ssa_ctx* c, ecdna_rep_summary_t* out_summaries,
             }
             std::vector<uint16_t> big;
             for (uint64_t i = 0; i < p.n_replicates; ++i) {
-                uint16_t* r = out_rows + i * c->row_stride;
+                uint16_t* r = out_rows + i * c->out_stride;
+                const uint16_t* dr = dev_rows.data() + i * c->row_stride;
                 uint64_t small = 0;
                 for (uint64_t b = 0; b < kb; ++b) small += bags[i * kb + b];
                 const uint64_t nbig = std::min<uint64_t>(summ[i].nplus >= small ? summ[i].nplus - small : 0,
                                                          c->row_stride);
-                big.assign(r, r + nbig);
+                big.assign(dr, dr + nbig);
                 uint64_t pos = 0;
                 for (uint64_t b = 0; b < kb; ++b)
-                    for (uint32_t q = 0; q < bags[i * kb + b] && pos < c->row_stride; ++q) r[pos++] = (uint16_t)(b + 1);
-                const uint64_t tail = std::min<uint64_t>(big.size(), c->row_stride - pos);
+                    for (uint32_t q = 0; q < bags[i * kb + b] && pos < c->out_stride; ++q) r[pos++] = (uint16_t)(b + 1);
+                const uint64_t tail = std::min<uint64_t>(big.size(), c->out_stride - pos);
                 std::copy(big.begin(), big.begin() + tail, r + pos);
             }
         }
@@ -697,7 +713,7 @@ int ecdna_ssa_ctx_download_snapshots(ecdna_ssa_ctx* c, ecdna_snapshot_t* meta, u
     if (meta) HIP_TRY(hipMemcpy(meta, c->d_snap_meta, ns * sizeof(ecdna_snapshot_t), hipMemcpyDeviceToHost));
     if (rows) {
         if (!c->d_snap_rows) return fail(ECDNA_E_STATE, "snapshot rows need ECDNA_FLAG_SNAPSHOT_ROWS");
-        HIP_TRY(hipMemcpy(rows, c->d_snap_rows, ns * c->row_stride * sizeof(uint16_t), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(rows, c->d_snap_rows, ns * c->out_stride * sizeof(uint16_t), hipMemcpyDeviceToHost));
     }
     return ECDNA_OK;
 }

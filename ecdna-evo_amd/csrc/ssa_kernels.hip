@@ -233,7 +233,7 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
                 m->taken = 1u;
                 m->reserved = 0u;
                 if (a.snap_rows) {
-                    uint16_t* dst = a.snap_rows + ((uint64_t)li * a.n_snap + sj) * a.row_stride;
+                    uint16_t* dst = a.snap_rows + ((uint64_t)li * a.n_snap + sj) * a.snap_stride;
                     const uint32_t hbm_end = WIN ? (wb < np ? wb : np) : np;
                     for (uint32_t j = 0; j < hbm_end; ++j) dst[j] = row[j];
                     if (WIN)
@@ -915,7 +915,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                     m->nplus = np;
                     m->taken = 1u;
                     m->reserved = 0u;
-                    if (a.snap_rows) expand(a.snap_rows + ((uint64_t)li * a.n_snap + sj) * a.row_stride, row, nb);
+                    if (a.snap_rows) expand(a.snap_rows + ((uint64_t)li * a.n_snap + sj) * a.snap_stride, row, nb);
                     ++sj;
                 }
             }
@@ -1000,6 +1000,15 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             // checked_mul panic (src/proliferation.rs:63-67), then the row-capacity check
             ev_err = (k > 32767u) ? (uint32_t)ECDNA_REP_ERR_OVERFLOW : ev_err;
             ev_err = (ev_err == 0u && un == 0u && np + 1u > a.cell_cap) ? (uint32_t)ECDNA_REP_ERR_CELL_CAP : ev_err;
+            // daughters (none for a death): [k1, k2] on an even split, [n] on an uneven one
+            const uint32_t da = (un == 0u) ? k1v : n;
+            const uint32_t db = n - k1v;
+            const bool has_a = prolif, has_b = prolif && un == 0u;
+            const bool sa = has_a && da <= K, sb = has_b && db <= K;
+            if (prolif && ev_err == 0u && ((has_a && !sa) || (has_b && !sb))) {  // room in the large-k row (rare)
+                const uint32_t nb_new = nb - (small ? 0u : 1u) + ((has_a && !sa) ? 1u : 0u) + ((has_b && !sb) ? 1u : 0u);
+                if (nb_new > rare_args()->big_cap) ev_err = ECDNA_REP_ERR_CELL_CAP;
+            }
             if (prolif && ev_err) {  // the event is not applied; the replicate stops (rare)
                 err = ev_err;
                 stop = ECDNA_STOP_ERROR;
@@ -1007,11 +1016,6 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             } else {
                 const double tau = softlog_neg(w.x, logtab) / a0;
 
-                // daughters (none for a death): [k1, k2] on an even split, [n] on an uneven one
-                const uint32_t da = (un == 0u) ? k1v : n;
-                const uint32_t db = n - k1v;
-                const bool has_a = prolif, has_b = prolif && un == 0u;
-                const bool sa = has_a && da <= K, sb = has_b && db <= K;
                 const uint32_t ns_old = ns;
                 // common case: every copy number involved is binned -> LDS only, no branch
                 // (bin_add masks its copy number into range, so lanes adding 0 need no select)

@@ -81,7 +81,7 @@ class Params(C.Structure):
         ("init_set_offsets", C.POINTER(C.c_uint32)),
         ("init_set_nminus", C.POINTER(C.c_uint64)),
         ("device", C.c_int32),
-        ("reserved1", C.c_int32),
+        ("big_cap", C.c_uint32),
         ("snapshot_cells", C.POINTER(C.c_uint64)),
         ("n_snapshots", C.c_uint32),
         ("replicate_stride", C.c_uint32),
@@ -173,6 +173,7 @@ class RunSpec:
     stats_target: Optional[Sequence[int]] = None  # target histogram [hist_bins] for ABC distances
     bin_kmax: int = 0  # FLAG_BIN_STORE: binned copy numbers 1..bin_kmax (0 = 64)
     set_cost_hint: Optional[Sequence[float]] = None  # per set: start costlier sets first (speed only)
+    big_cap: int = 0  # FLAG_BIN_STORE: large-k row capacity (cells with k > bin_kmax); 0 = cell_cap
     _keep: list = field(default_factory=list, repr=False)
 
     def replicate_ids(self) -> np.ndarray:
@@ -227,6 +228,7 @@ class RunSpec:
         p.max_iter = self.max_iter
         p.flags = self.flags
         p.bin_kmax = self.bin_kmax
+        p.big_cap = self.big_cap
         p.device = self.device
         if self.snapshots:
             snaps = np.asarray(sorted(int(x) for x in self.snapshots), dtype=np.uint64)

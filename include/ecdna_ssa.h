@@ -86,7 +86,8 @@ typedef enum {
     ECDNA_REP_OK = 0,
     ECDNA_REP_ERR_OVERFLOW = 1,   /* 2k > u16::MAX: checked_mul panic, src/proliferation.rs:63-67 */
     ECDNA_REP_ERR_EMPTY = 2,      /* empty initial distribution: ensure!, src/process.rs:88, 232 */
-    ECDNA_REP_ERR_CELL_CAP = 3,   /* N+ row would exceed cell_cap (the reference grows a Vec) */
+    ECDNA_REP_ERR_CELL_CAP = 3,   /* N+ row would exceed cell_cap (the reference grows a Vec), or the
+                                     bin store's large-k row would exceed big_cap */
     ECDNA_REP_ERR_REJECTION = 4   /* BinomialNoUneven loop exceeded 4096 redraws (p < 2^-4096) */
 } ecdna_rep_error_t;
 
@@ -156,7 +157,10 @@ typedef struct {
     const uint32_t* init_set_offsets; /* host or NULL */
     const uint64_t* init_set_nminus;  /* host or NULL */
     int32_t device;                 /* HIP device ordinal for ecdna_ssa_run / ctx_create */
-    int32_t reserved1;
+    uint32_t big_cap;               /* ECDNA_FLAG_BIN_STORE: capacity (cells) of a replicate's large-k row,
+                                       the cells with k > bin_kmax; 0 = cell_cap. A division that would put
+                                       more cells there stops the replicate with ECDNA_REP_ERR_CELL_CAP. The
+                                       device row memory is sized by it, outputs by cell_cap. */
     /* Snapshots (--snapshots, src/clap_app.rs:92-97, 102-134; SavingOptions, src/lib.rs:21-25): cell
      * counts, sorted ascending, at most 64. Before every event, while any REMAINING snapshot equals
      * n- + n+, the FRONT one is popped and the current state saved (src/process.rs:122-145, the

@@ -291,6 +291,7 @@ typedef struct {
     uint64_t ns;                  /* sum of c */
     uint16_t* big;                /* B */
     uint64_t nb;
+    uint64_t big_cap;             /* capacity of B (params big_cap, 0 = cell_cap) */
 } binstore;
 
 static void bins_add(binstore* b, uint32_t k) {
@@ -364,6 +365,11 @@ static int prolif_nplus_bins(binstore* b, uint64_t* nminus, uint64_t cap, wstrea
     int err = segregate(ws, seg, n, &k1, &uneven);
     if (err) return err;
     if (uneven == UNEVEN_FALSE && L + 1 > cap) return ECDNA_REP_ERR_CELL_CAP;
+    { /* room for the large daughters in B (ecdna_ssa_params_t.big_cap); a removed B cell frees its slot */
+        const uint64_t large = uneven == UNEVEN_FALSE ? (uint64_t)(k1 > b->K) + (uint64_t)(n - k1 > b->K)
+                                                       : (uint64_t)(n > b->K);
+        if (large && b->nb - (i >= b->ns ? 1u : 0u) + large > b->big_cap) return ECDNA_REP_ERR_CELL_CAP;
+    }
     if (uneven == UNEVEN_FALSE) {
         uint32_t d[2] = {k1, n - k1};
         bins_replace(b, i, k, d, 2);
@@ -473,6 +479,7 @@ static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16
     if (binned) {
         bs = calloc(1, sizeof(binstore));
         bs->K = p->bin_kmax ? p->bin_kmax : 64;
+        bs->big_cap = (p->big_cap && p->big_cap < p->cell_cap) ? p->big_cap : p->cell_cap;
         bs->big = malloc(((size_t)p->cell_cap + 1) * sizeof(uint16_t));
         for (uint64_t j = 0; j < nplus; ++j) bins_add(bs, init[j]);
         if (snap_rows) snap_scratch = malloc(((size_t)p->cell_cap + 1) * sizeof(uint16_t));
@@ -698,6 +705,17 @@ static int validate(const ecdna_ssa_params_t* p, uint64_t row_stride, int want_r
         if (!p->init_set_offsets) break;
     }
     if (maxn > p->cell_cap) return ECDNA_E_INVALID;
+    if ((p->flags & ECDNA_FLAG_BIN_STORE) && p->big_cap) { /* initial cells above bin_kmax fit in B */
+        const uint32_t kmax = p->bin_kmax ? p->bin_kmax : 64u;
+        for (uint32_t s = 0; s < p->n_param_sets; ++s) {
+            const uint16_t* c;
+            uint64_t np, nm, big = 0;
+            init_of_set(p, s, &c, &np, &nm);
+            for (uint64_t j = 0; j < np; ++j) big += c[j] > kmax;
+            if (big > p->big_cap) return ECDNA_E_INVALID;
+            if (!p->init_set_offsets) break;
+        }
+    }
     if ((p->flags & ECDNA_FLAG_BIN_STORE) && p->bin_kmax != 0 && p->bin_kmax != 32 && p->bin_kmax != 64 &&
         p->bin_kmax != 256)
         return ECDNA_E_INVALID;

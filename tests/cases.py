@@ -119,6 +119,15 @@ def bin_cases():
     c["bins256_boundary_bd"] = abi.RunSpec(seed=45, process=abi.BIRTH_DEATH, rates=((1.0, 1.3, 0.6, 0.7),),
                                            n_replicates=32, max_cells=500, init={250: 3, 257: 4, 600: 1},
                                            hist_bins=700, bin_kmax=256, flags=H | B)
+    # bounded large-k row (big_cap): device rows of 64 cells while outputs keep cell_cap's stride; 40-copy
+    # cells divide into two large daughters until the row is full (ECDNA_REP_ERR_CELL_CAP)
+    c["bins_big_cap_error"] = abi.RunSpec(seed=48, process=abi.BIRTH_DEATH, rates=((1.0, 1.3, 0.5, 0.5),),
+                                          n_replicates=32, max_cells=400, init={40: 6, 1: 4}, bin_kmax=32, big_cap=10,
+                                          hist_bins=300, flags=H | B)
+    c["bins_big_cap_snapshots"] = abi.RunSpec(seed=49, process=abi.BIRTH_DEATH, rates=((1.0, 1.2, 0.4, 0.4),),
+                                              n_replicates=32, max_cells=300, init={36: 3, 2: 5}, bin_kmax=32,
+                                              big_cap=200, hist_bins=300, snapshots=[10, 40, 120],
+                                              flags=H | B | abi.FLAG_SNAPSHOT_ROWS)
     c["bins_c32"] = abi.RunSpec(seed=46, process=abi.BIRTH_DEATH, rates=BD_RATES, n_replicates=32, max_cells=1500,
                                 cell_cap=70_000, init={1: 2, 70: 1}, flags=H | B)
     c["bins256_c32"] = abi.RunSpec(seed=47, process=abi.BIRTH_DEATH, rates=((1.0, 1.0, 0.9, 0.9),), n_replicates=16,

@@ -230,14 +230,15 @@ def test_c5_shard_full_size_properties(engine_mod, oracle_mod, store):
     """C5 rank-0 shard at full size (32,768 replicates, rows up to 1e6 cells = 2 MB, 65 GB of rows):
     invariants, bookkeeping, the stop law of a critical-ish turnover process, and replicates 0..3
     (about 2e7 events each) against the oracle bit for bit (event hash). The bin store runs its
-    256-bin, u32-counter variant here (cell_cap 1e6 > 65535)."""
-    kw = dict(flags=abi.FLAG_EVENT_HASH | STORES[store], bin_kmax=256 if store == "bins" else 0)
+    256-bin, u32-counter variant here (cell_cap 1e6 > 65535) with a large-k row of 2^14 cells."""
+    kw = dict(flags=abi.FLAG_EVENT_HASH | STORES[store], bin_kmax=256 if store == "bins" else 0,
+              big_cap=(1 << 14) if store == "bins" else 0)  # bins: a bounded large-k row (k > 256 is rare)
     spec = c5_shard_spec(**kw)
     r = engine_mod.run(spec)
     _invariants(r, spec)
     _balance(r, 1000)
     stops = set(r.summaries["stop_reason"].tolist())
-    assert stops <= {abi.STOP_MAX_CELLS, abi.STOP_MAX_TIME, abi.STOP_ABSORBING}, stops
+    assert stops <= {abi.STOP_MAX_CELLS, abi.STOP_MAX_TIME, abi.STOP_ABSORBING}, stops  # (no row-capacity errors)
     c = oracle_mod.run(c5_shard_spec(n_replicates=4, **kw), mode="philox", n_threads=4)
     for f in c.summaries.dtype.names:
         np.testing.assert_array_equal(r.summaries[f][:4], c.summaries[f], err_msg=f)

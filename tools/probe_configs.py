@@ -37,7 +37,7 @@ def c5_shard(rank=0, gpus=8):
     n = 262_144 // gpus
     return abi.RunSpec(seed=42, process=abi.BIRTH_DEATH, rates=((1.0, 1.0, 0.9, 0.9),), reps_per_set=262_144,
                        first_replicate=rank * n, n_replicates=n, max_cells=1_000_000, max_time=1000.0,
-                       init={1: 1000}, hist_bins=1025, flags=0)
+                       init={1: 1000}, hist_bins=1025, flags=0, big_cap=int(os.environ.get("PROBE_BIG_CAP", 1 << 16)))
 
 
 CONFIGS = {
