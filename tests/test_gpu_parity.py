@@ -8,6 +8,9 @@ import numpy as np
 import pytest
 
 from cases import bin_cases, cases
+from ecdna_evo_amd import abi
+
+H = abi.FLAG_EVENT_HASH
 
 CASES = cases()
 BIN_CASES = bin_cases()
@@ -135,3 +138,22 @@ def test_gpu_hbm_only_variant_matches_oracle(name, engine_mod, oracle_mod, monke
     monkeypatch.setenv("ECDNA_SSA_WINDOW", "0")
     spec = CASES[name]
     _compare(engine_mod.run(spec, want_rows=True), oracle_mod.run(spec, mode="philox", want_rows=True), name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flags", [H, H | abi.FLAG_BIN_STORE])
+def test_gpu_edge_sizes_match_oracle(flags, engine_mod, oracle_mod):
+    """Zero replicates, one replicate, and global ids at the top of the u64 range (Philox counter words
+    rid_hi = 0xffffffff, interleaved with a stride) against the oracle."""
+    empty = abi.RunSpec(seed=3, n_replicates=0, reps_per_set=1, max_cells=100, flags=flags)
+    r = engine_mod.run(empty)
+    assert len(r.summaries) == 0 and int(r.hist.sum()) == 0 and int(r.totals["replicates"].sum()) == 0
+    top = 2**64 - 1
+    for spec in (abi.RunSpec(seed=4, process=abi.BIRTH_DEATH, rates=((1.0, 1.5, 0.3, 0.3),), n_replicates=1,
+                             max_cells=2000, flags=flags),
+                 abi.RunSpec(seed=5, process=abi.BIRTH_DEATH, rates=((1.0, 1.5, 0.3, 0.3),),
+                             first_replicate=top - 1 - 3 * 36, n_replicates=37, replicate_stride=3, reps_per_set=top,
+                             max_cells=800, flags=flags)):
+        gpu = engine_mod.run(spec, want_rows=True)
+        cpu = oracle_mod.run(spec, mode="philox", want_rows=True)
+        _compare(gpu, cpu, f"edge/{spec.n_replicates}")
