@@ -212,6 +212,62 @@ __global__ void __launch_bounds__(256) k_cmp_s(uint32_t* out, uint32_t s) {
     if (r == 0x12345) out[0] = 1;
 }
 
+
+// v_cndmask_b32_e32 reading VCC (set once per 8), and v_cmp_*_e32 writing VCC
+__global__ void __launch_bounds__(256) k_cndmask_e32(uint32_t* out, uint32_t s) {
+    uint32_t v[8];
+    for (int j = 0; j < 8; ++j) v[j] = threadIdx.x + j;
+    for (int i = 0; i < ITERS; ++i) {
+        asm volatile(
+            "v_cmp_gt_u32_e32 vcc, %0, %8\n"
+            "v_cndmask_b32_e32 %0, %0, %8, vcc\n v_cndmask_b32_e32 %1, %1, %8, vcc\n"
+            "v_cndmask_b32_e32 %2, %2, %8, vcc\n v_cndmask_b32_e32 %3, %3, %8, vcc\n"
+            "v_cndmask_b32_e32 %4, %4, %8, vcc\n v_cndmask_b32_e32 %5, %5, %8, vcc\n"
+            "v_cndmask_b32_e32 %6, %6, %8, vcc\n v_cndmask_b32_e32 %7, %7, %8, vcc"
+            : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
+            : "v"(s) : "vcc");
+    }
+    uint32_t r = 0;
+    for (int j = 0; j < 8; ++j) r ^= v[j];
+    if (r == 0x12345) out[0] = r;
+}
+
+__global__ void __launch_bounds__(256) k_cmp_e32(uint32_t* out, uint32_t s) {
+    uint32_t v[8];
+    uint64_t acc = 0;
+    for (int j = 0; j < 8; ++j) v[j] = threadIdx.x + j;
+    for (int i = 0; i < ITERS; ++i) {
+        uint64_t m;
+        asm volatile(
+            "v_cmp_gt_u32_e32 vcc, %1, %9\n v_cmp_gt_u32_e32 vcc, %2, %9\n"
+            "v_cmp_gt_u32_e32 vcc, %3, %9\n v_cmp_gt_u32_e32 vcc, %4, %9\n"
+            "v_cmp_gt_u32_e32 vcc, %5, %9\n v_cmp_gt_u32_e32 vcc, %6, %9\n"
+            "v_cmp_gt_u32_e32 vcc, %7, %9\n v_cmp_gt_u32_e32 vcc, %8, %9\n s_mov_b64 %0, vcc"
+            : "=s"(m) : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]), "v"(s)
+            : "vcc");
+        acc ^= m;
+    }
+    if (acc == 0x12345) out[0] = 1;
+}
+
+// v_addc_co_u32_e32: add with the carry in and out through VCC (the borrow/carry counting idiom)
+__global__ void __launch_bounds__(256) k_addc_e32(uint32_t* out, uint32_t s) {
+    uint32_t v[8];
+    for (int j = 0; j < 8; ++j) v[j] = threadIdx.x + j;
+    for (int i = 0; i < ITERS; ++i) {
+        asm volatile(
+            "v_addc_co_u32_e32 %0, vcc, %0, %8, vcc\n v_addc_co_u32_e32 %1, vcc, %1, %8, vcc\n"
+            "v_addc_co_u32_e32 %2, vcc, %2, %8, vcc\n v_addc_co_u32_e32 %3, vcc, %3, %8, vcc\n"
+            "v_addc_co_u32_e32 %4, vcc, %4, %8, vcc\n v_addc_co_u32_e32 %5, vcc, %5, %8, vcc\n"
+            "v_addc_co_u32_e32 %6, vcc, %6, %8, vcc\n v_addc_co_u32_e32 %7, vcc, %7, %8, vcc"
+            : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
+            : "v"(s) : "vcc");
+    }
+    uint32_t r = 0;
+    for (int j = 0; j < 8; ++j) r ^= v[j];
+    if (r == 0x12345) out[0] = r;
+}
+
 template <typename F>
 void time_it(const char* name, F launch, double insts_per_lane_iter, int cus, double clk_hz) {
     hipEvent_t a, b;
@@ -293,5 +349,8 @@ int main() {
     time_it("mad_u64_v", [&] { hipLaunchKernelGGL(k_mad_u64_v, g, blk, 0, 0, d, 0xD2511F53u); }, 8, cus, clk);
     time_it("cndmask_e64_s", [&] { hipLaunchKernelGGL(k_cndmask_s, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
     time_it("cmp_e64_s", [&] { hipLaunchKernelGGL(k_cmp_s, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
+    time_it("cndmask_e32_vcc", [&] { hipLaunchKernelGGL(k_cndmask_e32, g, blk, 0, 0, d, 3u); }, 9, cus, clk);
+    time_it("cmp_e32_vcc", [&] { hipLaunchKernelGGL(k_cmp_e32, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
+    time_it("addc_e32_vcc", [&] { hipLaunchKernelGGL(k_addc_e32, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
     return 0;
 }
