@@ -56,7 +56,7 @@ struct StepperArgs {
     ecdna_snapshot_t* snap_meta;    // [n][n_snap], chunk-offset
     uint16_t* snap_rows;            // [n][n_snap][snap_stride] or nullptr, chunk-offset
     uint64_t snap_stride;           // cells per snapshot row (cell_cap rounded up)
-    uint32_t big_cap;               // bin store: large-k row capacity (<= row_stride)
+    uint32_t big_cap;               // bin store: large-k row capacity (<= cell_cap, <= row_stride)
     void* bags;                     // bin store: [n][bin_k] final u16 / u32 bin counters (chunk-local)
     // bin store drain control: waves in SIMD wave slots >= admit_slot (the youngest) take no fresh
     // replicate once fewer than admit_remaining are left; admit_slot = 0xffffffff: off
