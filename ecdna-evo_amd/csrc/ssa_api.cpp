@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -61,6 +62,11 @@ InitOfSet init_of_set(const ecdna_ssa_params_t* p, uint64_t s) {
 int validate(const ecdna_ssa_params_t* p) {
     if (!p) return fail(ECDNA_E_INVALID, "params is NULL");
     if (!p->rates || p->n_param_sets == 0) return fail(ECDNA_E_INVALID, "rates/n_param_sets");
+    for (uint32_t s = 0; s < p->n_param_sets; ++s) {  // (the steppers' time-step division relies on it)
+        const ecdna_rates_t& r = p->rates[s];
+        for (const float x : {r.b0, r.b1, r.d0, r.d1})
+            if (!(x >= 0.f && x <= FLT_MAX)) return fail(ECDNA_E_INVALID, "rates must be finite and >= 0");
+    }
     if (p->reps_per_set == 0) return fail(ECDNA_E_INVALID, "reps_per_set must be >= 1");
     if (p->hist_bins < 2 || p->hist_bins > ecdna::kMaxHistBins)
         return fail(ECDNA_E_INVALID, "hist_bins must be in [2, 4096]");

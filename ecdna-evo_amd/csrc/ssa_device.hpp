@@ -143,6 +143,21 @@ __device__ __forceinline__ double softlog_neg(uint32_t w, const double2* tab) {
     return -fma((double)(ex - 32), 0x1.62e42fefa39efp-1, cl.y + l);
 }
 
+// n / d, the correctly rounded IEEE quotient (the oracle's C division), for operands in the stepper's
+// range. LLVM lowers an f64 divide to v_div_scale x2, v_rcp_f64, two Newton steps, the quotient and its
+// residual, v_div_fmas and v_div_fixup; the scales, the scale flag of v_div_fmas and the fixup only act
+// when an operand or the quotient is near the denormal or overflow range, or on zero / inf / NaN
+// divisors. The time step divides a soft log in [2^-33, 23] (or 0) by a total propensity in
+// [2^-200, 2^162] (finite non-negative f32 rates, ecdna_ssa_ctx_create; u32 populations; a0 > 0), so
+// they are identities there and the same rcp / fma sequence without them yields the same bits.
+__device__ __forceinline__ double div_in_range(double n, double d) {
+    const double r0 = __builtin_amdgcn_rcp(d);
+    const double r1 = fma(r0, fma(-d, r0, 1.0), r0);
+    const double r2 = fma(r1, fma(-d, r1, 1.0), r1);
+    const double q = n * r2;
+    return fma(fma(-d, q, n), r2, q);
+}
+
 // The log table in constant memory; each workgroup stages it into LDS (divergent per-lane index).
 __constant__ const double kLogTab[2 * ECDNA_LOGTAB_N] = ECDNA_LOGTAB_INIT;
 

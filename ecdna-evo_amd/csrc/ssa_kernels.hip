@@ -346,7 +346,7 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
         }
 
         // waiting time
-        const double tau = softlog_neg(w.x, logtab) / a0;
+        const double tau = div_in_range(softlog_neg(w.x, logtab), a0);
 
         uint64_t x = ch;
         if (ch == 1u) {
@@ -428,6 +428,22 @@ __device__ unsigned long long g_rot_stats[12];
 #define ROT_STAT(i, v) __hip_atomic_fetch_add(&g_rot_stats[i], (unsigned long long)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
 #else
 #define ROT_STAT(i, v) ((void)0)
+#endif
+
+// Development counters of the bin stepper's rare blocks (built with -DECDNA_PATH_STATS only;
+// tools/path_stats.py): how many wave-iterations execute each block (the first active lane counts).
+#ifdef ECDNA_PATH_STATS
+__device__ unsigned long long g_path_stats[8];
+__device__ __forceinline__ void path_stat(int i, uint64_t v = 1) {
+    const uint64_t ex = __builtin_amdgcn_read_exec();
+    if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(ex))
+        __hip_atomic_fetch_add(&g_path_stats[i], (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#define PATH_STAT(i) path_stat(i)
+#define PATH_STAT_LANES(i) path_stat(i, (uint64_t)__builtin_popcountll(__builtin_amdgcn_read_exec()))
+#else
+#define PATH_STAT(i) ((void)0)
+#define PATH_STAT_LANES(i) ((void)0)
 #endif
 
 // The kernel argument block as seen from a rare path: read through a pointer the compiler cannot prove
@@ -882,6 +898,8 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
         if (any_bound) c_bound += clock64() - cb0;
 #endif
         if (!active) continue;  // (an empty initial distribution)
+        PATH_STAT(0);
+        PATH_STAT_LANES(1);
         const uint32_t np = ns + nb;
 
         // propensities rate_i * population_i over [n-, n+(, n-, n+)]
@@ -948,13 +966,17 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             // uniform N+ cell: Lemire multiply-shift on w2; exact rejection (rare) from the stream
             uint64_t m = mul_u32_wide(w.z, np);
             if (nplus_ev && (uint32_t)m < np) {
+                PATH_STAT(3);
                 const uint32_t thr = (0u - np) % np;
                 while ((uint32_t)m < thr) m = (uint64_t)ws.next() * np;
             }
             const uint32_t idx = (uint32_t)(m >> 32);
             const bool small = idx < ns;
             uint32_t k = bin_find(small ? idx : 0u);
-            if (nplus_ev && !small) k = gload_u16_l2(row + (idx - ns));  // large-k row (rare)
+            if (nplus_ev && !small) {  // large-k row (rare)
+                PATH_STAT(4);
+                k = gload_u16_l2(row + (idx - ns));
+            }
 
             // Exponential::increase_nplus (src/proliferation.rs:25-111): its draws and error checks
             const uint32_t n = 2u * k;
@@ -971,6 +993,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                 k1v = __popc(w.w & (uint32_t)m64) + __popc(sp0 & (uint32_t)(m64 >> 32));
                 if (prolif && fast) ws.pos = fast1 ? 2u : 3u;
                 if (prolif && !fast && k <= 32767u) {  // larger copy numbers or a rejected pick: more words
+                    PATH_STAT(5);
                     k1v = ws.binomial_half(n, &rk);
                     if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN) {
                         uint32_t tries = 1;
@@ -1009,6 +1032,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             // np + 1 <= big_cap: one compare on the event path, the checks themselves in a rare block
             // (C3: 88.0 ms per launch without any big_cap check, 91.8 with it on every event, 89.3 gated).
             if (np + 1u > a.big_cap) {
+                PATH_STAT(7);
                 KArgs* const ra = rare_args();
                 if (prolif && ev_err == 0u && un == 0u && np + 1u > ra->cell_cap) ev_err = ECDNA_REP_ERR_CELL_CAP;
                 const uint32_t nb_new = nb - (small ? 0u : 1u) + ((has_a && !sa) ? 1u : 0u) + ((has_b && !sb) ? 1u : 0u);
@@ -1020,7 +1044,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                 stop = ECDNA_STOP_ERROR;
                 active = false;
             } else {
-                const double tau = softlog_neg(w.x, logtab) / a0;
+                const double tau = div_in_range(softlog_neg(w.x, logtab), a0);
 
                 const uint32_t ns_old = ns;
                 // common case: every copy number involved is binned -> LDS only, no branch
@@ -1030,6 +1054,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
                 bin_add(db, sb ? 1u : 0u);
                 ns = ns - ((nplus_ev && small) ? 1u : 0u) + (sa ? 1u : 0u) + (sb ? 1u : 0u);
                 if (nplus_ev && (!small || (has_a && !sa) || (has_b && !sb))) {  // the large-k row (rare)
+                    PATH_STAT(6);
                     uint32_t open = small ? 0xffffffffu : idx - ns_old;  // B slot freed by a large picked cell
                     if (has_a && !sa) {
                         if (open != 0xffffffffu) {
@@ -1302,6 +1327,14 @@ hipError_t launch_hist(const HistArgs& a, uint32_t blocks, hipStream_t stream) {
 
 }  // namespace ecdna
 
+#ifdef ECDNA_PATH_STATS
+// Development: read (and reset) the rare-block counters of the last launches (tools/path_stats.py)
+extern "C" int ecdna_dev_path_stats(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ecdna::g_path_stats), sizeof(ecdna::g_path_stats)) != hipSuccess) return -1;
+    unsigned long long z[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(ecdna::g_path_stats), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 #ifdef ECDNA_ROT_STATS
 // Development: read (and reset) the rotation counters of the last launches (tools/rot_stats.py)
 extern "C" int ecdna_dev_rot_stats(unsigned long long* out) {

@@ -117,7 +117,8 @@ typedef enum {
 #define ECDNA_E_STATE (-5)     /* call order (e.g. download before launch) */
 
 /* Rates of one parameter set: ReactionRates([b0, b1, d0, d1]) (src/main.rs:67, 139). f32 as in Cli
- * (src/clap_app.rs:41-55). */
+ * (src/clap_app.rs:41-55). Each must be finite and >= 0 (else ECDNA_E_INVALID; the reference does not
+ * check them). */
 typedef struct {
     float b0, b1, d0, d1;
 } ecdna_rates_t;

@@ -31,6 +31,7 @@
 #include "ssa_oracle.h"
 #include "ssa_logtab.h"
 
+#include <float.h>
 #include <math.h>
 #include <pthread.h>
 #include <stdatomic.h>
@@ -687,6 +688,11 @@ static void* worker(void* arg) {
 static int validate(const ecdna_ssa_params_t* p, uint64_t row_stride, int want_rows) {
     if (!p || !p->rates || p->n_param_sets == 0 || p->reps_per_set == 0 || p->hist_bins < 2)
         return ECDNA_E_INVALID;
+    for (uint32_t s = 0; s < p->n_param_sets; ++s) { /* finite, non-negative rates */
+        const float x[4] = {p->rates[s].b0, p->rates[s].b1, p->rates[s].d0, p->rates[s].d1};
+        for (int i = 0; i < 4; ++i)
+            if (!(x[i] >= 0.f && x[i] <= FLT_MAX)) return ECDNA_E_INVALID;
+    }
     if (p->process != ECDNA_PURE_BIRTH && p->process != ECDNA_BIRTH_DEATH) return ECDNA_E_INVALID;
     if (p->segregation < 0 || p->segregation > 3) return ECDNA_E_INVALID;
     if (p->max_iter > 0xffffffffull) return ECDNA_E_INVALID;

@@ -114,7 +114,10 @@ def test_invalid_parameters_rejected(product_lib):
     bad.append(s2.params())
     s3 = abi.RunSpec(rates=((1, 1, 0, 0), (1, 2, 0, 0)), reps_per_set=2, n_replicates=8)
     bad.append(s3.params())  # replicate 7 -> set 3 >= 2 sets
-    keep = [s, s2, s3]  # noqa: F841  (host arrays referenced by the params)
+    bad_rates = [abi.RunSpec(rates=(r,), n_replicates=4) for r in
+                 ((1, float("inf"), 0, 0), (1, 1, float("nan"), 0), (1, 1, 0, -0.5), (-1e-30, 1, 0, 0))]
+    bad += [r.params() for r in bad_rates]  # rates must be finite and >= 0
+    keep = [s, s2, s3, bad_rates]  # noqa: F841  (host arrays referenced by the params)
     for q in bad:
         h = C.c_void_p()
         rc = product_lib.ecdna_ssa_ctx_create(C.byref(q), C.byref(h))
@@ -153,3 +156,11 @@ def test_set_cost_hint_in_params():
     with pytest.raises(ValueError):
         abi.RunSpec(rates=((1, 1, 0, 0),), set_cost_hint=[1.0, 2.0]).params()
     assert C.sizeof(abi.Params) % 8 == 0
+
+
+def test_oracle_rejects_invalid_rates(oracle_mod):
+    """The oracle keeps the product's contract: rates finite and >= 0 (include/ecdna_ssa.h)."""
+    for r in ((1, float("inf"), 0, 0), (1, 1, float("nan"), 0), (1, 1, 0, -0.5)):
+        with pytest.raises(ValueError):
+            oracle_mod.run(abi.RunSpec(rates=(r,), n_replicates=2, max_cells=10))
+    oracle_mod.run(abi.RunSpec(rates=((0, 3.0e38, 0, 1e-45),), n_replicates=2, max_cells=10))

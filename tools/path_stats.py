@@ -1,0 +1,31 @@
+"""Rare-block counters of the bin stepper over one C3 launch (development tool). Needs a library built
+with -DECDNA_PATH_STATS (EXTRA=-DECDNA_PATH_STATS bash tools/ab_build.sh WORKTREE pstats), selected with
+ECDNA_SSA_LIB. Prints wave-iterations, active lanes, and per rare block the fraction of wave-iterations
+that execute it (at least one lane in the block)."""
+import ctypes as C
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ecdna-evo_amd"))
+from ecdna_evo_amd import abi, engine  # noqa: E402
+
+spec = abi.RunSpec(seed=42, process=abi.BIRTH_DEATH, rates=((1.0, 1.5, 0.3, 0.3),), n_replicates=1 << 20,
+                   max_cells=10_000, flags=abi.FLAG_BIN_STORE, bin_kmax=32)
+lib = engine.lib()
+fn = lib.ecdna_dev_path_stats
+fn.argtypes = [C.POINTER(C.c_ulonglong)]
+ctx = engine.Context(spec)
+buf = (C.c_ulonglong * 8)()
+names = ["wave_iters", "lane_iters", "-", "lemire_reject", "large_pick", "binomial_words", "large_row_update",
+         "capacity_gate"]
+for rep in range(2):
+    fn(buf)
+    ctx.launch()
+    ms, _ = ctx.sync()
+    fn(buf)
+    d = {k: int(v) for k, v in zip(names, buf)}
+    w = max(d["wave_iters"], 1)
+    frac = {k: round(d[k] / w, 5) for k in names[3:]}
+    print(json.dumps({"ms": ms, **d, "lanes_per_wave_iter": round(d["lane_iters"] / w, 2),
+                      "fraction_of_wave_iters": frac}), flush=True)
