@@ -287,6 +287,33 @@ void time_it(const char* name, F launch, double insts_per_lane_iter, int cus, do
            per_simd_cycle, clk_hz / 1e6, wave_insts / (ms * 1e-3));
 }
 
+// round 2 (r02e): what makes the VOP2 select slow — the encoding, the VCC read, or the VALU write of VCC
+#define SEL8(fmt)                                                                                        \
+    asm volatile(fmt(0) fmt(1) fmt(2) fmt(3) fmt(4) fmt(5) fmt(6) fmt(7)                                \
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),     \
+                   "+v"(v[7])                                                                           \
+                 : "v"(s), "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), \
+                   "v"(x[7])                                                                            \
+                 : "vcc")
+#define E64_VCC(j) "v_cndmask_b32_e64 %" #j ", %" #j ", %8, vcc\n"
+#define E32_VCC(j) "v_cndmask_b32_e32 %" #j ", %" #j ", %8, vcc\n"
+#define E32_MIX(j) "v_cndmask_b32_e32 %" #j ", %" #j ", %8, vcc\n v_xor_b32 %" #j ", %" #j ", %8\n"
+#define XOR_ONLY(j) "v_xor_b32 %" #j ", %" #j ", %8\n v_xor_b32 %" #j ", %" #j ", %8\n"
+#define SELKERNEL(name, FMT, SETVCC)                                                                     \
+    __global__ void __launch_bounds__(256) name(uint32_t* out, uint32_t s) {                             \
+        uint32_t v[8], x[8];                                                                             \
+        for (int j = 0; j < 8; ++j) v[j] = threadIdx.x + j, x[j] = threadIdx.x * 3u + j;                \
+        asm volatile(SETVCC ::: "vcc");                                                                  \
+        for (int i = 0; i < ITERS; ++i) SEL8(FMT);                                                       \
+        uint32_t r = 0;                                                                                  \
+        for (int j = 0; j < 8; ++j) r ^= v[j];                                                           \
+        if (r == 0x12345) out[0] = r;                                                                    \
+    }
+SELKERNEL(k_sel_e64_vcc, E64_VCC, "s_mov_b64 vcc, 0x5555aaaa")
+SELKERNEL(k_sel_e32_svcc, E32_VCC, "s_mov_b64 vcc, 0x5555aaaa")
+SELKERNEL(k_sel_e32_mix, E32_MIX, "s_mov_b64 vcc, 0x5555aaaa")
+SELKERNEL(k_sel_xor_only, XOR_ONLY, "s_mov_b64 vcc, 0x5555aaaa")
+
 int main() {
     hipDeviceProp_t p;
     hipGetDeviceProperties(&p, 0);
@@ -351,6 +378,10 @@ int main() {
     time_it("cmp_e64_s", [&] { hipLaunchKernelGGL(k_cmp_s, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
     time_it("cndmask_e32_vcc", [&] { hipLaunchKernelGGL(k_cndmask_e32, g, blk, 0, 0, d, 3u); }, 9, cus, clk);
     time_it("cmp_e32_vcc", [&] { hipLaunchKernelGGL(k_cmp_e32, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
+    time_it("sel_e64_vcc", [&] { hipLaunchKernelGGL(k_sel_e64_vcc, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
+    time_it("sel_e32_svcc", [&] { hipLaunchKernelGGL(k_sel_e32_svcc, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
+    time_it("sel_e32_mix", [&] { hipLaunchKernelGGL(k_sel_e32_mix, g, blk, 0, 0, d, 3u); }, 16, cus, clk);
+    time_it("sel_xor_only", [&] { hipLaunchKernelGGL(k_sel_xor_only, g, blk, 0, 0, d, 3u); }, 16, cus, clk);
     time_it("addc_e32_vcc", [&] { hipLaunchKernelGGL(k_addc_e32, g, blk, 0, 0, d, 3u); }, 8, cus, clk);
     return 0;
 }
