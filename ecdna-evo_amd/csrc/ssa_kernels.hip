@@ -434,16 +434,24 @@ __device__ unsigned long long g_rot_stats[12];
 // tools/path_stats.py): how many wave-iterations execute each block (the first active lane counts).
 #ifdef ECDNA_PATH_STATS
 __device__ unsigned long long g_path_stats[8];
-__device__ __forceinline__ void path_stat(int i, uint64_t v = 1) {
-    const uint64_t ex = __builtin_amdgcn_read_exec();
-    if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(ex))
-        __hip_atomic_fetch_add(&g_path_stats[i], (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-#define PATH_STAT(i) path_stat(i)
-#define PATH_STAT_LANES(i) path_stat(i, (uint64_t)__builtin_popcountll(__builtin_amdgcn_read_exec()))
+// counts in registers (the first active lane of the block adds 1, or the active-lane count), summed into
+// g_path_stats once per lane at exit
+#define PATH_STAT(i) (ps[i] += ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec())) ? 1u : 0u)
+#define PATH_STAT_LANES(i)                                                                                      \
+    do {                                                                                                        \
+        const uint64_t ex_ = __builtin_amdgcn_read_exec();                                                      \
+        const uint32_t pc_ = __builtin_amdgcn_readfirstlane((uint32_t)__builtin_popcountll(ex_));              \
+        ps[i] += ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(ex_)) ? pc_ : 0u;                          \
+    } while (0)
+#define PATH_STATS_DECL uint32_t ps[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}
+#define PATH_STATS_FLUSH()                                                                                      \
+    for (int q = 0; q < 8; ++q)                                                                               \
+        if (ps[q]) __hip_atomic_fetch_add(&g_path_stats[q], (unsigned long long)ps[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
 #else
 #define PATH_STAT(i) ((void)0)
 #define PATH_STAT_LANES(i) ((void)0)
+#define PATH_STATS_DECL
+#define PATH_STATS_FLUSH() ((void)0)
 #endif
 
 // The kernel argument block as seen from a rare path: read through a pointer the compiler cannot prove
@@ -544,6 +552,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
     const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
     const PhiloxKeys rk = philox_round_keys(k0, k1);  // event blocks: round keys in VGPRs
     PhiloxEventPre pre{0u, 0u, 0u};  // the replicate-only part of round 0
+    PATH_STATS_DECL;
     const uint32_t stop32 = a.stop_cells < 0xffffffffull ? (uint32_t)a.stop_cells : 0xffffffffu;
 
     // packed counter add: bin b (0-based, copy number b + 1) / group g, by +d (d = +1, -1 or 0, as a
@@ -1094,6 +1103,7 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
             }
         }
     }
+    PATH_STATS_FLUSH();
 #ifdef ECDNA_ROT_STATS
     if ((threadIdx.x & 63u) == 0u) {
         ROT_STAT(8, c_tick);
