@@ -135,6 +135,7 @@ struct ecdna_ssa_ctx {
     // per-replicate final counters [chunk_reps][bin_k]
     uint32_t bin_k = 0;
     int bin_c32 = 0;
+    int bin_ilp = 0;  // the bin stepper's max-ILP schedule (lone waves; ssa_launch.h)
     void* d_bags = nullptr;
     uint32_t stepper_block = ecdna::kStepperBlock;
     // owned copies of the host inputs
@@ -428,9 +429,18 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
     c->window = env_u64("ECDNA_SSA_WINDOW", 1) ? 1 : 0;
     int per_cu = 0;
     if (c->bin_k) {
+        // Instruction schedule: with at most one wave of replicates per SIMD (every chunk within 256 lanes
+        // per CU) each wave runs alone and waits on its own dependencies, and the max-ILP schedule is faster
+        // (C2 8.6 -> 8.1 ms, C5 8-GPU shard 22.0 -> 21.1 s); with more, issue binds and the default schedule
+        // keeps 4 waves per SIMD (max-ILP: 3, C3 +8 %). ECDNA_SSA_SCHED = 0 default, 1 max-ILP, 2 auto.
+        uint64_t max_chunk = 0;
+        for (const auto& ch : c->chunks) max_chunk = std::max<uint64_t>(max_chunk, ch.n);
+        const uint64_t sched = env_u64("ECDNA_SSA_SCHED", 2);
+        c->bin_ilp = sched == 1 || (sched == 2 && max_chunk <= (uint64_t)c->cus * 256u);
         // bin store: LDS-resident events, bounded by issue and LDS latency: every resident block helps
         CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per_cu, ecdna::bin_stepper_kernel(p->process, p->segregation, c->bin_k, c->bin_c32, p->flags),
+            &per_cu,
+            ecdna::bin_stepper_kernel(p->process, p->segregation, c->bin_k, c->bin_c32, p->flags, c->bin_ilp),
             (int)c->stepper_block, 0));
     } else {
         CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -577,7 +587,7 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
 
         HIP_TRY(hipEventRecord(ch.ev[0], st));
         if (c->bin_k)
-            HIP_TRY(ecdna::launch_bin_stepper(a, p.process, p.segregation, c->bin_k, c->bin_c32, blocks, st));
+            HIP_TRY(ecdna::launch_bin_stepper(a, p.process, p.segregation, c->bin_k, c->bin_c32, c->bin_ilp, blocks, st));
         else
             HIP_TRY(ecdna::launch_stepper(a, p.process, p.segregation, c->window, blocks, st));
         HIP_TRY(hipEventRecord(ch.ev[1], st));

@@ -422,9 +422,19 @@ struct BinLayout {
 // plain load), so a stale cached copy can never hide a waiting replicate.
 constexpr int kCpolSc1 = 16;  // buffer cache policy: sc1 (gfx940+ bit 4)
 
+// The second instruction schedule of the bin stepper (ECDNA_ILP_BUILD: this file compiled again with
+// -mllvm -amdgpu-sched-strategy=max-ilp, Makefile): only its bin-stepper table and accessor are defined
+// there (template argument SCH = 1 keeps its kernels distinct from this build's SCH = 0 ones). Its
+// development counters are its own (static): the tools read the default build's.
+#ifdef ECDNA_ILP_BUILD
+#define ECDNA_DEV_STATIC static
+#else
+#define ECDNA_DEV_STATIC
+#endif
+
 // Development counters of the rotation (built with -DECDNA_ROT_STATS only; tools/rot_stats.py)
 #ifdef ECDNA_ROT_STATS
-__device__ unsigned long long g_rot_stats[12];
+ECDNA_DEV_STATIC __device__ unsigned long long g_rot_stats[12];
 #define ROT_STAT(i, v) __hip_atomic_fetch_add(&g_rot_stats[i], (unsigned long long)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
 #else
 #define ROT_STAT(i, v) ((void)0)
@@ -433,7 +443,7 @@ __device__ unsigned long long g_rot_stats[12];
 // Development counters of the bin stepper's rare blocks (built with -DECDNA_PATH_STATS only;
 // tools/path_stats.py): how many wave-iterations execute each block (the first active lane counts).
 #ifdef ECDNA_PATH_STATS
-__device__ unsigned long long g_path_stats[8];
+ECDNA_DEV_STATIC __device__ unsigned long long g_path_stats[8];
 // counts in registers (the first active lane of the block adds 1, or the active-lane count), summed into
 // g_path_stats once per lane at exit
 #define PATH_STAT(i) (ps[i] += ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec())) ? 1u : 0u)
@@ -540,7 +550,7 @@ __device__ __forceinline__ uint32_t vec_get(const uint4& v, int j) {
     return (w[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
 }
 
-template <bool BD, int SEG, int NG, bool C32, int BLK, int TF>
+template <bool BD, int SEG, int NG, bool C32, int BLK, int TF, int SCH>  // SCH: the build's schedule (no code)
 __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
     using L = BinLayout<NG, C32>;
     constexpr uint32_t K = L::kK;
@@ -1271,6 +1281,7 @@ __global__ void __launch_bounds__(kHistBlock) ssa_hist(const HistArgs a) {
 
 // ---------------------------------------------------------------- launch
 
+#ifndef ECDNA_ILP_BUILD
 #define ECDNA_STEPPER_TABLE(BD, WIN)                                                                        \
     {(const void*)ssa_stepper<BD, 0, WIN>, (const void*)ssa_stepper<BD, 1, WIN>,                             \
      (const void*)ssa_stepper<BD, 2, WIN>, (const void*)ssa_stepper<BD, 3, WIN>}
@@ -1278,16 +1289,22 @@ __global__ void __launch_bounds__(kHistBlock) ssa_hist(const HistArgs a) {
 static const void* const kStepperTable[2][2][4] = {
     {ECDNA_STEPPER_TABLE(false, false), ECDNA_STEPPER_TABLE(true, false)},
     {ECDNA_STEPPER_TABLE(false, true), ECDNA_STEPPER_TABLE(true, true)}};
+#endif
 
-// bin-store variants: [birth_death][segregation][K = 64 | 256][u16 | u32 counters]; the 256-bin
-// u32 variant runs 64-lane blocks (its 72 KiB of LDS per 64 lanes)
+// bin-store variants: [birth_death][segregation][K = 32 | 64 | 256][u16 | u32 counters]; the 256-bin
+// u32 variant runs 64-lane blocks (its 72 KiB of LDS per 64 lanes); this build's schedule (SCH)
+#ifdef ECDNA_ILP_BUILD
+#define ECDNA_SCH 1
+#else
+#define ECDNA_SCH 0
+#endif
 #define ECDNA_BIN_SEG(BD, SEG, TF)                                                                         \
-    {{(const void*)ssa_stepper_bins<BD, SEG, 4, false, kStepperBlock, TF>,                                  \
-      (const void*)ssa_stepper_bins<BD, SEG, 4, true, kStepperBlock, TF>},                                  \
-     {(const void*)ssa_stepper_bins<BD, SEG, 8, false, kStepperBlock, TF>,                                  \
-      (const void*)ssa_stepper_bins<BD, SEG, 8, true, kStepperBlock, TF>},                                  \
-     {(const void*)ssa_stepper_bins<BD, SEG, 32, false, kBinWideBlock, TF>,                                 \
-      (const void*)ssa_stepper_bins<BD, SEG, 32, true, kBinWideBlock, TF>}}
+    {{(const void*)ssa_stepper_bins<BD, SEG, 4, false, kStepperBlock, TF, ECDNA_SCH>,                       \
+      (const void*)ssa_stepper_bins<BD, SEG, 4, true, kStepperBlock, TF, ECDNA_SCH>},                       \
+     {(const void*)ssa_stepper_bins<BD, SEG, 8, false, kStepperBlock, TF, ECDNA_SCH>,                       \
+      (const void*)ssa_stepper_bins<BD, SEG, 8, true, kStepperBlock, TF, ECDNA_SCH>},                       \
+     {(const void*)ssa_stepper_bins<BD, SEG, 32, false, kBinWideBlock, TF, ECDNA_SCH>,                      \
+      (const void*)ssa_stepper_bins<BD, SEG, 32, true, kBinWideBlock, TF, ECDNA_SCH>}}
 #define ECDNA_BIN_TABLE(BD, TF) \
     {ECDNA_BIN_SEG(BD, 0, TF), ECDNA_BIN_SEG(BD, 1, TF), ECDNA_BIN_SEG(BD, 2, TF), ECDNA_BIN_SEG(BD, 3, TF)}
 
@@ -1295,14 +1312,24 @@ static const void* const kStepperTable[2][2][4] = {
 static const void* const kBinStepperTable[2][2][4][3][2] = {{ECDNA_BIN_TABLE(false, 0), ECDNA_BIN_TABLE(true, 0)},
                                                             {ECDNA_BIN_TABLE(false, 1), ECDNA_BIN_TABLE(true, 1)}};
 
+static const void* bin_table_entry(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags) {
+    const int tf = (flags & (ECDNA_FLAG_TIME_F32 | ECDNA_FLAG_EVENT_HASH)) ? 1 : 0;
+    return kBinStepperTable[tf][birth_death ? 1 : 0][segregation & 3][bin_k > 64 ? 2 : (bin_k > 32 ? 1 : 0)]
+                           [c32 ? 1 : 0];
+}
+
+#ifdef ECDNA_ILP_BUILD
+const void* bin_stepper_kernel_ilp(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags) {
+    return bin_table_entry(birth_death, segregation, bin_k, c32, flags);
+}
+#else
 const void* stepper_kernel(int birth_death, int segregation, int window) {
     return kStepperTable[window ? 1 : 0][birth_death ? 1 : 0][segregation & 3];
 }
 
-const void* bin_stepper_kernel(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags) {
-    const int tf = (flags & (ECDNA_FLAG_TIME_F32 | ECDNA_FLAG_EVENT_HASH)) ? 1 : 0;
-    return kBinStepperTable[tf][birth_death ? 1 : 0][segregation & 3][bin_k > 64 ? 2 : (bin_k > 32 ? 1 : 0)]
-                           [c32 ? 1 : 0];
+const void* bin_stepper_kernel(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags, int ilp) {
+    return ilp ? bin_stepper_kernel_ilp(birth_death, segregation, bin_k, c32, flags)
+               : bin_table_entry(birth_death, segregation, bin_k, c32, flags);
 }
 
 int bin_stepper_block(uint32_t bin_k) { return bin_k > 64 ? kBinWideBlock : kStepperBlock; }
@@ -1315,11 +1342,11 @@ hipError_t launch_stepper(const StepperArgs& a, int birth_death, int segregation
                            0, stream);
 }
 
-hipError_t launch_bin_stepper(const StepperArgs& a, int birth_death, int segregation, uint32_t bin_k, int c32,
+hipError_t launch_bin_stepper(const StepperArgs& a, int birth_death, int segregation, uint32_t bin_k, int c32, int ilp,
                               uint32_t blocks, hipStream_t stream) {
     StepperArgs copy = a;
     void* args[] = {&copy};
-    return hipLaunchKernel(bin_stepper_kernel(birth_death, segregation, bin_k, c32, a.flags), dim3(blocks),
+    return hipLaunchKernel(bin_stepper_kernel(birth_death, segregation, bin_k, c32, a.flags, ilp), dim3(blocks),
                            dim3(bin_stepper_block(bin_k)), args, 0, stream);
 }
 
@@ -1334,10 +1361,11 @@ hipError_t launch_hist(const HistArgs& a, uint32_t blocks, hipStream_t stream) {
     const int bag = a.bags ? (a.bag_c32 ? 2 : 1) : 0;
     return hipLaunchKernel(table[a.stats ? 1 : 0][bag], dim3(blocks), dim3(kHistBlock), args, lds, stream);
 }
+#endif  // ECDNA_ILP_BUILD
 
 }  // namespace ecdna
 
-#ifdef ECDNA_PATH_STATS
+#if defined(ECDNA_PATH_STATS) && !defined(ECDNA_ILP_BUILD)
 // Development: read (and reset) the rare-block counters of the last launches (tools/path_stats.py)
 extern "C" int ecdna_dev_path_stats(unsigned long long* out) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ecdna::g_path_stats), sizeof(ecdna::g_path_stats)) != hipSuccess) return -1;
@@ -1345,7 +1373,7 @@ extern "C" int ecdna_dev_path_stats(unsigned long long* out) {
     return hipMemcpyToSymbol(HIP_SYMBOL(ecdna::g_path_stats), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif
-#ifdef ECDNA_ROT_STATS
+#if defined(ECDNA_ROT_STATS) && !defined(ECDNA_ILP_BUILD)
 // Development: read (and reset) the rotation counters of the last launches (tools/rot_stats.py)
 extern "C" int ecdna_dev_rot_stats(unsigned long long* out) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ecdna::g_rot_stats), sizeof(ecdna::g_rot_stats)) != hipSuccess) return -1;

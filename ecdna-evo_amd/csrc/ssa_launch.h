@@ -112,9 +112,13 @@ hipError_t launch_stepper(const StepperArgs& a, int birth_death, int segregation
 // Bin store (ECDNA_FLAG_BIN_STORE): bin_k = 64 or 256 binned copy numbers; c32 = u32 counters
 // (cell_cap > 65535); flags selects the compile-time variant without f32 time and event hash when
 // neither is set. bin_stepper_block = the variant's workgroup size.
-const void* bin_stepper_kernel(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags);
+// ilp: 1 = the max-ILP instruction schedule of the same kernels (a second compile of ssa_kernels.hip,
+// ECDNA_ILP_BUILD): fewer stalls for lone waves, more VGPRs (3 waves per SIMD); the ABI takes it when a
+// chunk has at most one wave of replicates per SIMD.
+const void* bin_stepper_kernel(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags, int ilp);
+const void* bin_stepper_kernel_ilp(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags);
 int bin_stepper_block(uint32_t bin_k);
-hipError_t launch_bin_stepper(const StepperArgs& a, int birth_death, int segregation, uint32_t bin_k, int c32,
+hipError_t launch_bin_stepper(const StepperArgs& a, int birth_death, int segregation, uint32_t bin_k, int c32, int ilp,
                               uint32_t blocks, hipStream_t stream);
 hipError_t launch_hist(const HistArgs& a, uint32_t blocks, hipStream_t stream);
 

@@ -171,3 +171,15 @@ def test_gpu_extreme_rates_match_oracle(flags, engine_mod, oracle_mod):
                            max_cells=400, init={1: 2, 40: 1}, max_time=float("inf"), flags=flags)
         _compare(engine_mod.run(spec, want_rows=True), oracle_mod.run(spec, mode="philox", want_rows=True),
                  f"rates {rates}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sched", ["0", "1"])
+@pytest.mark.parametrize("name", sorted(BIN_CASES))
+def test_gpu_bin_store_both_schedules_match_oracle(name, sched, engine_mod, oracle_mod, monkeypatch):
+    """The bin stepper's two instruction schedules (ECDNA_SSA_SCHED: 0 = occupancy-first, the large-run
+    default; 1 = max-ILP, taken automatically for at most one wave of replicates per SIMD, i.e. for every
+    case here) are the same kernels: both bit for bit against the oracle."""
+    monkeypatch.setenv("ECDNA_SSA_SCHED", sched)
+    spec = BIN_CASES[name]
+    _compare(engine_mod.run(spec, want_rows=True), oracle_mod.run(spec, mode="philox", want_rows=True), name)

@@ -15,5 +15,9 @@ for f in csrc/ssa_kernels.hip csrc/ssa_api.cpp; do
   x=""; [ "${f##*.}" = cpp ] && x="-x hip"
   /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -ffp-contract=off ${EXTRA:-} $x -c "$f" -o "$TMP/$(basename "$f").o"
 done
+if grep -q ECDNA_ILP_BUILD csrc/ssa_kernels.hip; then  # (refs since the two-schedule build)
+  /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -ffp-contract=off ${EXTRA:-} -DECDNA_ILP_BUILD \
+    -mllvm -amdgpu-sched-strategy=max-ilp -c csrc/ssa_kernels.hip -o "$TMP/ssa_kernels_ilp.o"
+fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libecdna_ssa.so" "$TMP"/*.o
 echo "$OUT/libecdna_ssa.so"

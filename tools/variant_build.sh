@@ -11,5 +11,7 @@ mkdir -p "$OUT"
 cd "$ROOT/ecdna-evo_amd"
 /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -ffp-contract=off "$@" -c csrc/ssa_kernels.hip -o "$TMP/k.o"
 /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -ffp-contract=off "$@" -x hip -c csrc/ssa_api.cpp -o "$TMP/a.o"
+/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -ffp-contract=off "$@" -DECDNA_ILP_BUILD \
+  -mllvm -amdgpu-sched-strategy=max-ilp -c csrc/ssa_kernels.hip -o "$TMP/ki.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libecdna_ssa.so" "$TMP"/*.o
 echo "$OUT/libecdna_ssa.so"
