@@ -39,6 +39,7 @@ import json
 import os
 import sys
 import time
+from typing import Optional
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "ecdna-evo_amd"))
@@ -83,9 +84,18 @@ def valu_measured_ceilings():
 BENCH_BIN_KMAX = 32
 
 
+# bin_kmax per workload (measured): K = 32 where the pick scan dominates (C3 issue-bound: 5 %
+# faster than 64; C2), K = 64 where copy numbers spread (C4: k0 up to 128, 8-GPU makespan 156 -> 131 ms;
+# C5: 1e6 cells)
+WORKLOAD_KMAX = {"c2": 32, "c3": BENCH_BIN_KMAX, "c4": 64, "c5": 64}
+
+
 def workload_spec(first: int, n: int, total: int, seed: int = 42, device: int = 0, store: str = "bins",
-                  bin_kmax: int = BENCH_BIN_KMAX, workload: str = "c3", stride: int = 1) -> abi.RunSpec:
-    """Replicates first, first + stride, ... (n of them) of the workload's `total` (SURVEY.md §8d shapes)."""
+                  bin_kmax: Optional[int] = None, workload: str = "c3", stride: int = 1) -> abi.RunSpec:
+    """Replicates first, first + stride, ... (n of them) of the workload's `total` (SURVEY.md §8d shapes);
+    bin_kmax None = the workload's default (WORKLOAD_KMAX)."""
+    if bin_kmax is None:
+        bin_kmax = WORKLOAD_KMAX[workload]
     common = dict(seed=seed, first_replicate=first, n_replicates=n, replicate_stride=stride, hist_bins=1025,
                   flags=abi.FLAG_BIN_STORE if store == "bins" else 0, device=device)
     if workload == "c3":
@@ -101,11 +111,10 @@ def workload_spec(first: int, n: int, total: int, seed: int = 42, device: int = 
         d = dict(process=abi.BIRTH_DEATH, rates=rates, reps_per_set=total // 1024, max_cells=10_000,
                  init_per_set=inits, set_cost_hint=abi.cost_hint(rates, inits))  # costly sets start first
     elif workload == "c5":
-        # broad copy numbers at 1e6 cells: K = 64; the large-k row holds at most 2^16 cells (128 KB
-        # per replicate instead of cell_cap's 2 MB, so the 262,144 replicates fit in HBM in one chunk)
+        # the large-k row holds at most 2^16 cells (128 KB per replicate instead of cell_cap's 2 MB, so the
+        # 262,144 replicates fit in HBM in one chunk)
         d = dict(process=abi.BIRTH_DEATH, rates=((1.0, 1.0, 0.9, 0.9),), reps_per_set=total, max_cells=1_000_000,
                  max_time=1000.0, init={1: 1000}, big_cap=1 << 16 if store == "bins" else 0)
-        bin_kmax = 64
     else:
         raise ValueError(workload)
     return abi.RunSpec(segregation=abi.SEG_BINOMIAL, bin_kmax=bin_kmax if store == "bins" else 0, **common, **d)
@@ -203,7 +212,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--reps-per-gpu", type=int, default=REPS_PER_GPU)
     ap.add_argument("--store", choices=("bins", "rows"), default="bins")
-    ap.add_argument("--bin-kmax", type=int, choices=(32, 64, 256), default=BENCH_BIN_KMAX)
+    ap.add_argument("--bin-kmax", type=int, choices=(32, 64, 256), default=None,
+                    help="bin store K (default: the workload's, WORKLOAD_KMAX)")
     ap.add_argument("--dump-hist", default="", help="rank 0 saves the reduced histogram and totals (.npz)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3",
                     help="BASELINE.json config; c3 (default) is the metric's weak-scaling line")

@@ -1,12 +1,12 @@
 #!/bin/bash
 # All eight C4 shards (ABC sweep, 8-GPU layout) one after another on this GPU: the 8-GPU makespan is the
-# slowest shard. PROBE_SHARD=interleaved (default) or contiguous; K = 32.
+# slowest shard. PROBE_SHARD=interleaved (default) or contiguous; K = 64 (PROBE_KMAX).
 # Usage: [PROBE_SHARD=contiguous] bash tools/c4_shards.sh
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 O=gpurun_out/c4_shards_${PROBE_SHARD:-interleaved}.log; : > $O
 for r in 0 1 2 3 4 5 6 7; do
-  PROBE_RANK=$r PROBE_FLAGS=0x20 PROBE_KMAX=${PROBE_KMAX:-32} timeout -k 10 120 python3 tools/probe_configs.py c4 | grep "^{" >> $O
+  PROBE_RANK=$r PROBE_FLAGS=0x20 PROBE_KMAX=${PROBE_KMAX:-64} timeout -k 10 120 python3 tools/probe_configs.py c4 | grep "^{" >> $O
 done
 python3 -c "
 import json
