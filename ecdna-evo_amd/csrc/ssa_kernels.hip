@@ -426,6 +426,16 @@ constexpr int kCpolSc1 = 16;  // buffer cache policy: sc1 (gfx940+ bit 4)
 // -mllvm -amdgpu-sched-strategy=max-ilp, Makefile): only its bin-stepper table and accessor are defined
 // there (template argument SCH = 1 keeps its kernels distinct from this build's SCH = 0 ones). Its
 // development counters are its own (static): the tools read the default build's.
+#ifndef ECDNA_FF_MAX
+#define ECDNA_FF_MAX 16
+#endif
+#ifndef ECDNA_FF_ENTER8
+#define ECDNA_FF_ENTER8 7  // enter when >= this many eighths of the lanes expect an N- event w.p. >= ECDNA_FF_ENTER8 / 8
+#endif
+#ifndef ECDNA_FF_STAY8
+#define ECDNA_FF_STAY8 7   // keep going while >= this many eighths of the entered lanes do
+#endif
+constexpr uint32_t kFfMax = ECDNA_FF_MAX;  // N- fast-forward: events per full iteration at most
 #ifdef ECDNA_ILP_BUILD
 #define ECDNA_DEV_STATIC static
 #else
@@ -720,11 +730,14 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
     const uint32_t tick_mask = rot ? ((1u << a.rot_tick_log2) - 1u) : 0xffffffffu;
     uint32_t it = 0;
     bool pinned = false;
+    uint32_t ff_tick = 0;  // N- fast-forward: iterations (wave-uniform) and the wave's mode
+    bool ff_mode = false;
 
 #ifdef ECDNA_ROT_STATS
     unsigned long long c_tick = 0, c_bound = 0, c_start = clock64();
 #endif
     for (;;) {
+        ++ff_tick;
         if (rot && ((++it & tick_mask) == 0u)) {  // ---- rotation tick (wave-uniform)
 #ifdef ECDNA_ROT_STATS
             const unsigned long long c0 = clock64();
@@ -916,6 +929,60 @@ __global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
 #ifdef ECDNA_ROT_STATS
         if (any_bound) c_bound += clock64() - cb0;
 #endif
+        // ---- N- fast-forward (birth-death; DESIGN.md §5 "N- fast-forward"): an N- event
+        // (ProliferateNMinus, DeathNMinus) picks no cell, so its exact work is the propensities, the stop
+        // checks, the block, the channel, the time step and the n- / spare / count / hash updates. While
+        // most of the wave's lanes draw N- events, they run them here, up to kFfMax per iteration, without
+        // the pick, the segregation and the counter updates. A lane leaves at its first N+ event or stop
+        // condition, untouched: the full event below draws that same event. Snapshots (checked per
+        // event) keep the full loop. The entry test runs every 8th iteration while the wave is not
+        // fast-forwarding, every iteration while it is (wave-uniform control: ballots at the loop top).
+        if (BD && kFfMax && !a.n_snap && (ff_mode || (ff_tick & 7u) == 0u)) {
+            const uint32_t npf = ns + nb;  // n+ is fixed during N- events
+            const double fpf = (double)npf;
+            const double pbf = rb1 * fpf, pdf = rd1 * fpf;
+            const double pm = rb0 * (double)nm + rd0 * (double)nm;
+            const bool heavy = active && pm * 8.0 >= (pm + pbf + pdf) * (double)ECDNA_FF_ENTER8;
+            const uint32_t n_in = (uint32_t)__builtin_popcountll(__ballot(active));
+            ff_mode = n_in != 0u && (uint32_t)__builtin_popcountll(__ballot(heavy)) * 8u >= n_in * ECDNA_FF_ENTER8;
+            if (ff_mode) {
+                bool go = active;
+#pragma unroll 1
+                for (uint32_t q = 0; q < kFfMax; ++q) {
+                    if ((uint32_t)__builtin_popcountll(__ballot(go)) * 8u < n_in * ECDNA_FF_STAY8) break;  // (uniform)
+                    if (go) {
+                        const double fm2 = (double)nm;
+                        const double cA2 = rb0 * fm2;
+                        const double cB2 = cA2 + pbf;
+                        const double cC2 = cB2 + rd0 * fm2;
+                        const double a02 = cC2 + pdf;
+                        const bool t_over2 = f32t ? (t32 >= a.max_time32) : (t >= a.max_time);
+                        if ((e >= a.max_iter) || nm + npf >= stop32 || t_over2 || !(a02 > 0.0)) {
+                            go = false;
+                        } else {
+                            const uint4 w2 = philox_event(e, pre, rk);
+                            const double target2 = fma3((double)w2.y, 0x1p-32, 0x1p-33) * a02;
+                            const uint32_t ch2 = (target2 >= cA2 ? 1u : 0u) + (target2 >= cB2 ? 1u : 0u) +
+                                                 (target2 >= cC2 ? 1u : 0u);
+                            if (ch2 & 1u) {
+                                go = false;
+                            } else {
+                                const double tau2 = div_in_range(softlog_neg(w2.x, logtab), a02);
+                                spares_update(0u, w2.z, w2.w, sp0, sp1, nsp);
+                                nm = nm + (ch2 == 0u ? 1u : 0u) - (ch2 == 2u ? 1u : 0u);
+                                n_dm += ch2 == 2u ? 1u : 0u;
+                                e += 1;
+                                if (f32t)
+                                    t32 = t32 + (float)tau2;
+                                else
+                                    t = t + tau2;
+                                if (hash_on) h = (h ^ (uint64_t)ch2) * kFnvPrime;
+                            }
+                        }
+                    }
+                }
+            }
+        }
         if (!active) continue;  // (an empty initial distribution)
         PATH_STAT(0);
         PATH_STAT_LANES(1);

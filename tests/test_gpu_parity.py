@@ -183,3 +183,46 @@ def test_gpu_bin_store_both_schedules_match_oracle(name, sched, engine_mod, orac
     monkeypatch.setenv("ECDNA_SSA_SCHED", sched)
     spec = BIN_CASES[name]
     _compare(engine_mod.run(spec, want_rows=True), oracle_mod.run(spec, mode="philox", want_rows=True), name)
+
+
+def _nminus_heavy_specs():
+    """Populations that become mostly N- (N- fitter than N+; uneven splits of k = 1 cells feed it), so the
+    N- fast-forward runs most events; stops that land inside it (max_iter, max_time,
+    cells); both processes, K = 32 / 64 / 256, f32 time, the event hash on and off."""
+    out = {}
+    for i, (proc, rates, extra) in enumerate([
+            (abi.BIRTH_DEATH, (1.6, 1.0, 0.3, 0.3), dict(max_cells=3000)),
+            (abi.BIRTH_DEATH, (1.0, 1.0, 0.9, 0.9), dict(max_cells=5000, init={1: 40})),
+            (abi.PURE_BIRTH, (2.0, 1.0, 0.0, 0.0), dict(max_cells=2500)),
+            (abi.BIRTH_DEATH, (1.6, 1.0, 0.3, 0.3), dict(max_cells=100_000, max_iter=900)),
+            (abi.BIRTH_DEATH, (1.6, 1.0, 0.3, 0.3), dict(max_cells=100_000, max_time=4.5)),
+            (abi.BIRTH_DEATH, (1.6, 1.0, 0.3, 0.3), dict(max_cells=3000, flags_extra=abi.FLAG_TIME_F32)),
+    ]):
+        for kmax in (32, 64, 256):
+            for hash_ in (0, H):
+                d = dict(extra)
+                fx = d.pop("flags_extra", 0)
+                d.setdefault("init", {1: 3})
+                out[f"ff{i}_k{kmax}_h{int(bool(hash_))}"] = abi.RunSpec(
+                    seed=90 + i, process=proc, rates=(rates,), n_replicates=700, bin_kmax=kmax,
+                    flags=abi.FLAG_BIN_STORE | hash_ | fx, **d)
+    return out
+
+
+FF_SPECS = _nminus_heavy_specs()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(FF_SPECS))
+def test_gpu_nminus_fast_forward_matches_oracle(name, engine_mod, oracle_mod, monkeypatch):
+    """The bin stepper's N- fast-forward (birth-death runs) against the oracle, bit for bit,
+    on N--dominated runs, under both instruction schedules. (The pure-birth case has no fast-forward.)"""
+    spec = FF_SPECS[name]
+    cpu = oracle_mod.run(spec, mode="philox", want_rows=True)
+    for sched in ("1", "0"):
+        monkeypatch.setenv("ECDNA_SSA_SCHED", sched)
+        _compare(engine_mod.run(spec, want_rows=True), cpu, f"{name}/sched{sched}")
+    s = cpu.summaries
+    ev = s["events_by_type"].astype(np.int64)
+    nminus_share = (ev[:, 0] + ev[:, 2]).sum() / ev.sum()
+    assert nminus_share > 0.6, nminus_share  # the fast-forward's regime
