@@ -53,3 +53,13 @@ def test_workload_sample_runs_on_the_oracle(oracle_mod, workload):
         assert np.all(s["iters"][full] == 10_000 - 1)
     if workload == "c5":  # 1,000 initial cells; the run ends at 1e6 cells or extinction
         assert s["stop_reason"][0] in (abi.STOP_MAX_CELLS, abi.STOP_ABSORBING)
+
+
+@pytest.mark.parametrize("workload,kmax", [("c2", 32), ("c3", 32), ("c4", 64), ("c5", 64)])
+def test_workload_bin_kmax_defaults(workload, kmax):
+    """bench.py's K per workload (K = 32 where the pick scan dominates, 64 where copy numbers
+    spread); an explicit --bin-kmax overrides it; the row store has no K."""
+    total = bench.WORKLOADS[workload][0]
+    assert bench.workload_spec(0, 8, total, workload=workload).bin_kmax == kmax
+    assert bench.workload_spec(0, 8, total, workload=workload, bin_kmax=256).bin_kmax == 256
+    assert bench.workload_spec(0, 8, total, workload=workload, store="rows").bin_kmax == 0
