@@ -45,3 +45,61 @@ def reduce_outputs(hist, totals, group=None) -> None:
 
     dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
     dist.all_reduce(totals, op=dist.ReduceOp.SUM, group=group)
+
+
+def rank_ids(rank: int, world: int, total: int, layout: str):
+    """The global replicate ids a rank owns under `layout`, as a slice of range(total): "contiguous"
+    (shard_range), "interleaved" (interleaved_range) or "weak" (weak_range with total // world each)."""
+    if layout == "contiguous":
+        first, n = shard_range(rank, world, total)
+        return slice(first, first + n)
+    if layout == "interleaved":
+        first, n, stride = interleaved_range(rank, world, total)
+        return slice(first, first + n * stride, stride)
+    if layout == "weak":
+        first, n = weak_range(rank, total // world)
+        return slice(first, first + n)
+    raise ValueError(f"unknown shard layout {layout!r}")
+
+
+def gather_records(local, total: int, layout: str = "contiguous", group=None):
+    """All-gather per-replicate records into global replicate order on every rank.
+
+    `local` is a [n_local, W] tensor of this rank's records in its own order (row i = the i-th id of
+    rank_ids), on the process group's device (CUDA for RCCL, CPU for gloo). The ABC sweep's rejection
+    step (abc.md:38-55) needs every replicate's statistics in one place; this is the one exchange it
+    adds beside the histogram all-reduce (a gather of R/G records per rank). Shards differ
+    by at most one record, so each rank pads to the largest and one all_gather moves them."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    ids = [range(total)[rank_ids(r, world, total, layout)] for r in range(world)]
+    if local.shape[0] != len(ids[rank]):
+        raise ValueError(f"rank {rank} holds {local.shape[0]} records, its shard has {len(ids[rank])}")
+    width = tuple(local.shape[1:])
+    cap = max(len(x) for x in ids)
+    padded = torch.zeros((cap,) + width, dtype=local.dtype, device=local.device)
+    padded[: local.shape[0]] = local
+    parts = [torch.empty_like(padded) for _ in range(world)]
+    dist.all_gather(parts, padded, group=group)
+    out = torch.empty((sum(len(x) for x in ids),) + width, dtype=local.dtype, device=local.device)
+    for r in range(world):
+        out[rank_ids(r, world, total, layout)] = parts[r][: len(ids[r])]
+    return out
+
+
+def gather_structured(arr, total: int, layout: str = "contiguous", device=None, group=None):
+    """gather_records for a numpy structured array (ecdna_rep_summary_t or ecdna_rep_stats_t records as
+    abi.SUMMARY_DTYPE / abi.STATS_DTYPE): the records travel as raw bytes, so every field comes back
+    bit for bit. `device`: where the exchange buffers live ("cuda" under RCCL, None = CPU for gloo)."""
+    import numpy as np
+    import torch
+
+    raw = np.ascontiguousarray(arr).view(np.uint8).reshape(len(arr), arr.dtype.itemsize)
+    t = torch.from_numpy(raw.copy())
+    if device is not None:
+        t = t.to(device)
+    g = gather_records(t, total, layout, group).cpu().numpy()
+    return np.ascontiguousarray(g).view(arr.dtype).reshape(-1)

@@ -51,6 +51,10 @@ def _worker(rank, world, total, port, outdir, mode):
     tot = torch.from_numpy(r.totals.view(np.uint64).astype(np.int64).reshape(-1).copy())
     shard.reduce_outputs(hist, tot)
     np.save(os.path.join(outdir, f"summ{rank}.npy"), r.summaries)
+    # the ABC step's exchange: every replicate's record in global order on every rank
+    layout = {"strong": "contiguous", "interleaved": "interleaved", "weak": "weak"}[mode]
+    gathered = shard.gather_structured(r.summaries, total, layout)
+    np.save(os.path.join(outdir, f"gathered{rank}.npy"), gathered)
     if rank == 0:
         np.save(os.path.join(outdir, "hist.npy"), hist.numpy())
         np.save(os.path.join(outdir, "tot.npy"), tot.numpy())
@@ -74,6 +78,10 @@ def test_two_rank_shards_reduce_to_single_run(oracle_mod, tmp_path, mode):
         summ = np.concatenate(parts)
     for f in full.summaries.dtype.names:
         np.testing.assert_array_equal(summ[f], full.summaries[f])
+    for r in range(world):  # shard.gather_structured: bit-identical records in global id order on each rank
+        g = np.load(tmp_path / f"gathered{r}.npy")
+        assert g.dtype == full.summaries.dtype and len(g) == total
+        assert g.tobytes() == full.summaries.tobytes()
 
 
 def test_interleaved_calls_equal_one_call_per_set(oracle_mod):
@@ -108,3 +116,38 @@ def test_shard_ranges_partition():
             for (f0, n0), (f1, _) in zip(rs, rs[1:]):
                 assert f0 + n0 == f1
             assert sum(n for _, n in rs) == total
+
+
+def _gather_worker(rank, world, total, port, outdir, layout):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ids = np.arange(total)[shard.rank_ids(rank, world, total, layout)]
+    # records derived from the global id (f64, two columns), so the expected gather is known
+    local = torch.from_numpy(np.stack([ids * 0.5, -ids.astype(np.float64)], axis=1))
+    out = shard.gather_records(local, total, layout)
+    np.save(os.path.join(outdir, f"g{rank}.npy"), out.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("layout,total", [("contiguous", 7), ("interleaved", 7), ("interleaved", 2), ("weak", 6)])
+def test_three_rank_gather_records_ragged(tmp_path, layout, total):
+    """Ragged shards (7 records over 3 ranks; a rank with none when total < world) come back in global
+    id order on every rank."""
+    world = 3
+    mp.spawn(_gather_worker, args=(world, total, _free_port(), str(tmp_path), layout), nprocs=world, join=True)
+    ids = np.arange(total, dtype=np.float64)
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / f"g{r}.npy"), np.stack([ids * 0.5, -ids], axis=1))
+
+
+def test_rank_ids_partition():
+    for layout in ("contiguous", "interleaved"):
+        for total in (0, 1, 7, 1000):
+            for world in (1, 2, 3, 8):
+                ids = np.sort(np.concatenate([np.arange(total)[shard.rank_ids(r, world, total, layout)]
+                                              for r in range(world)]))
+                np.testing.assert_array_equal(ids, np.arange(total))
+    with pytest.raises(ValueError):
+        shard.rank_ids(0, 2, 10, "blocks")
