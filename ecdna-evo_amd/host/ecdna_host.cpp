@@ -23,7 +23,16 @@ std::map<uint32_t, uint64_t> Distribution::histogram() const {
 }
 
 Distribution Distribution::from_histogram(const std::map<uint32_t, uint64_t>& h) {
+    // the engine counts cells in u32 (include/ecdna_ssa.h: initial N- and N+ below 2^32); checked before
+    // anything is expanded, so a corrupt count fails here instead of in a terabyte allocation
+    uint64_t cells = 0;
+    for (const auto& kv : h) {
+        if (kv.second > 0xffffffffull) throw IoError("cell count " + std::to_string(kv.second) + " does not fit u32");
+        if (kv.first != 0) cells += kv.second;
+    }
+    if (cells > 0xffffffffull) throw IoError("more than 2^32 - 1 N+ cells");
     Distribution d;
+    d.nplus.reserve(cells);
     for (const auto& kv : h) {
         if (kv.first == 0) {
             d.nminus = kv.second;
@@ -86,6 +95,7 @@ Distribution from_json(const std::string& t) {
         skip_ws(t, i);
         uint64_t v = parse_uint(t, i);
         if (k > 65535) throw IoError("copy number " + std::to_string(k) + " does not fit u16");
+        if (v > ~0ull - h[(uint32_t)k]) throw IoError("cell count overflows u64 at offset " + std::to_string(i));
         h[(uint32_t)k] += v;
         skip_ws(t, i);
         if (i < t.size() && t[i] == ',') {

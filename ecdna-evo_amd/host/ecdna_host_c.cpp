@@ -35,9 +35,9 @@ int ecdna_host_subsample(const uint16_t* nplus, uint64_t n_plus, uint64_t nminus
     try {
         ecdna::host::Distribution d;
         d.nminus = nminus;
-        d.nplus.assign(nplus, nplus + n_plus);
+        if (n_plus) d.nplus.assign(nplus, nplus + n_plus);
         ecdna::host::Distribution s = ecdna::host::subsample(d, nb_cells, seed, rid, sample_index);
-        std::memcpy(out_nplus, s.nplus.data(), s.nplus.size() * sizeof(uint16_t));
+        if (!s.nplus.empty()) std::memcpy(out_nplus, s.nplus.data(), s.nplus.size() * sizeof(uint16_t));
         *out_n_plus = s.nplus.size();
         *out_nminus = s.nminus;
         return 0;
@@ -64,7 +64,7 @@ int64_t ecdna_host_load(const char* path, uint16_t* out_nplus, uint64_t cap, uin
     try {
         ecdna::host::Distribution d = ecdna::host::load_json(path);
         if (d.nplus.size() > cap) return -1;
-        std::memcpy(out_nplus, d.nplus.data(), d.nplus.size() * sizeof(uint16_t));
+        if (!d.nplus.empty()) std::memcpy(out_nplus, d.nplus.data(), d.nplus.size() * sizeof(uint16_t));
         *out_nminus = d.nminus;
         return (int64_t)d.nplus.size();
     } catch (...) {

@@ -138,6 +138,30 @@ def test_save_and_load_roundtrip(host, tmp_path):
     assert n == 6 and nm.value == 4 and list(out[:n]) == [1, 1, 1, 3, 3, 20]
 
 
+@pytest.mark.parametrize("body,want", [
+    ('{"0": 5}', (0, 5)),                       # N- only
+    ("{}", (0, 0)),                             # empty (the engine then reports the empty-distribution error)
+    ('{"0":1,"2":2,"2":1}', (3, 1)),            # a repeated key adds up
+    ('{"1": 4294967296}', -1),                  # more than 2^32 - 1 cells: refused before any allocation
+    ('{"1": 3000000000, "2": 3000000000}', -1),
+    ('{"0": 18446744073709551615, "0": 1}', -1),  # u64 overflow of a repeated key
+    ('{"1": 99999999999999999999}', -1),        # out of u64
+    ('{"65536": 1}', -1),                       # copy number beyond u16
+    ('{"1": 2,}', -1), ('{"1" 2}', -1), ('["1", 2]', -1), ("", -1),
+    ('{"1": 17}', -1),                          # more N+ cells than the caller's buffer (cap 16)
+])
+def test_load_rejects_malformed(host, tmp_path, body, want):
+    p = tmp_path / "d.json"
+    p.write_text(body)
+    out = np.zeros(16, np.uint16)
+    nm = C.c_uint64()
+    n = host.ecdna_host_load(str(p).encode(), out.ctypes.data, 16, C.byref(nm))
+    if want == -1:
+        assert n == -1
+    else:
+        assert (n, nm.value) == want
+
+
 def _philox(ctr, key):
     M0, M1, W0, W1 = 0xD2511F53, 0xCD9E8D57, 0x9E3779B9, 0xBB67AE85
     c = list(ctr)
