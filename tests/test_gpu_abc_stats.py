@@ -19,15 +19,19 @@ def _target(bins):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("store,kmax", [("rows", 0), ("bins", 32), ("bins", 64), ("bins", 256)])
 @pytest.mark.parametrize("with_target", [False, True])
-def test_rep_stats_match_restatement(engine_mod, oracle_mod, with_target):
+def test_rep_stats_match_restatement(engine_mod, oracle_mod, with_target, store, kmax):
+    """Both cell stores (the bin store's statistics read its counters and its large-k row: the initial
+    300-copy cell lies above every K)."""
     import abc_stats
 
     bins = 257
     tgt = _target(bins) if with_target else None
+    flags = abi.FLAG_REP_STATS | abi.FLAG_EVENT_HASH | (abi.FLAG_BIN_STORE if store == "bins" else 0)
     spec = abi.RunSpec(seed=4, process=abi.BIRTH_DEATH, rates=((1.0, 1.4, 0.3, 0.3), (1.0, 2.0, 0.5, 0.2)),
                        reps_per_set=300, n_replicates=600, max_cells=2000, hist_bins=bins, init={1: 3, 300: 1},
-                       stats_target=tgt, flags=abi.FLAG_REP_STATS | abi.FLAG_EVENT_HASH)
+                       stats_target=tgt, flags=flags, bin_kmax=kmax)
     g = engine_mod.run(spec)
     c = oracle_mod.run(spec, want_rows=True)
     np.testing.assert_array_equal(g.summaries["event_hash"], c.summaries["event_hash"])
