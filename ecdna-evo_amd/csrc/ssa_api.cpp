@@ -135,7 +135,7 @@ struct ecdna_ssa_ctx {
     // per-replicate final counters [chunk_reps][bin_k]
     uint32_t bin_k = 0;
     int bin_c32 = 0;
-    int bin_ilp = 0;  // the bin stepper's max-ILP schedule (lone waves; ssa_launch.h)
+    int bin_ilp = 0;  // the bin stepper's schedule: 0 default, 1 max-ILP (lone waves), 2 128-VGPR K = 64 (ssa_launch.h)
     void* d_bags = nullptr;
     uint32_t stepper_block = ecdna::kStepperBlock;
     // owned copies of the host inputs
@@ -432,11 +432,23 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
         // Instruction schedule: with at most one wave of replicates per SIMD (every chunk within 256 lanes
         // per CU) each wave runs alone and waits on its own dependencies, and the max-ILP schedule is faster
         // (C2 8.6 -> 8.1 ms, C5 8-GPU shard 22.0 -> 21.1 s); with more, issue binds and the default schedule
-        // keeps 4 waves per SIMD (max-ILP: 3, C3 +8 %). ECDNA_SSA_SCHED = 0 default, 1 max-ILP, 2 auto.
+        // keeps 4 waves per SIMD (max-ILP: 3, C3 +8 %). The K = 64 / u16 kernel needs 130 VGPRs (3
+        // workgroups per CU); its 128-VGPR build fits 4 and pays once lanes run many replicates each (the
+        // whole C4 sweep on one GPU, 16 per lane: 834 -> 771 ms) but not with few (C4 8-GPU shard, 2 per
+        // lane: a longer drain, 127 -> 134 ms), so auto takes it from 4 replicates per lane of its grid on.
+        // ECDNA_SSA_SCHED = 0 default, 1 max-ILP, 2 auto, 3 the 128-VGPR build (K = 64 / u16; else 0).
         uint64_t max_chunk = 0;
         for (const auto& ch : c->chunks) max_chunk = std::max<uint64_t>(max_chunk, ch.n);
         const uint64_t sched = env_u64("ECDNA_SSA_SCHED", 2);
-        c->bin_ilp = sched == 1 || (sched == 2 && max_chunk <= (uint64_t)c->cus * 256u);
+        // (auto only without f32 time and the event hash: that variant spills 12 B at 128 VGPRs)
+        const bool k64u16 = c->bin_k == 64 && !c->bin_c32;
+        const bool tf0 = (p->flags & (ECDNA_FLAG_TIME_F32 | ECDNA_FLAG_EVENT_HASH)) == 0;
+        if (sched == 1 || (sched == 2 && max_chunk <= (uint64_t)c->cus * 256u))
+            c->bin_ilp = 1;
+        else if (k64u16 && (sched == 3 || (sched == 2 && tf0 && max_chunk >= 4ull * c->cus * 4u * ecdna::kStepperBlock)))
+            c->bin_ilp = 2;
+        else
+            c->bin_ilp = 0;
         // bin store: LDS-resident events, bounded by issue and LDS latency: every resident block helps
         CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &per_cu,

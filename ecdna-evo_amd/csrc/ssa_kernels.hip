@@ -560,8 +560,10 @@ __device__ __forceinline__ uint32_t vec_get(const uint4& v, int j) {
     return (w[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
 }
 
-template <bool BD, int SEG, int NG, bool C32, int BLK, int TF, int SCH>  // SCH: the build's schedule (no code)
-__global__ void __launch_bounds__(BLK) ssa_stepper_bins(const StepperArgs a) {
+// SCH: the build's schedule (no code): 0 occupancy-first, 1 max-ILP (ECDNA_ILP_BUILD), 2 occupancy-first
+// capped at 128 VGPRs so that four 256-lane workgroups fit a CU (K = 64 / u16 only, many replicates per lane)
+template <bool BD, int SEG, int NG, bool C32, int BLK, int TF, int SCH>
+__global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const StepperArgs a) {
     using L = BinLayout<NG, C32>;
     constexpr uint32_t K = L::kK;
     __shared__ uint4 cnt_v[L::kBinVecs][BLK];  // bin counters
@@ -1385,6 +1387,17 @@ static const void* bin_table_entry(int birth_death, int segregation, uint32_t bi
                            [c32 ? 1 : 0];
 }
 
+#ifndef ECDNA_ILP_BUILD
+// K = 64 / u16 under a 128-VGPR cap (SCH = 2): [TF][birth_death][segregation]
+#define ECDNA_BIN_OCC4(BD, TF)                                                                               \
+    {(const void*)ssa_stepper_bins<BD, 0, 8, false, kStepperBlock, TF, 2>,                                   \
+     (const void*)ssa_stepper_bins<BD, 1, 8, false, kStepperBlock, TF, 2>,                                   \
+     (const void*)ssa_stepper_bins<BD, 2, 8, false, kStepperBlock, TF, 2>,                                   \
+     (const void*)ssa_stepper_bins<BD, 3, 8, false, kStepperBlock, TF, 2>}
+static const void* const kBinOcc4Table[2][2][4] = {{ECDNA_BIN_OCC4(false, 0), ECDNA_BIN_OCC4(true, 0)},
+                                                   {ECDNA_BIN_OCC4(false, 1), ECDNA_BIN_OCC4(true, 1)}};
+#endif
+
 #ifdef ECDNA_ILP_BUILD
 const void* bin_stepper_kernel_ilp(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags) {
     return bin_table_entry(birth_death, segregation, bin_k, c32, flags);
@@ -1395,8 +1408,12 @@ const void* stepper_kernel(int birth_death, int segregation, int window) {
 }
 
 const void* bin_stepper_kernel(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags, int ilp) {
-    return ilp ? bin_stepper_kernel_ilp(birth_death, segregation, bin_k, c32, flags)
-               : bin_table_entry(birth_death, segregation, bin_k, c32, flags);
+    if (ilp == 2 && bin_k == 64 && !c32) {
+        const int tf = (flags & (ECDNA_FLAG_TIME_F32 | ECDNA_FLAG_EVENT_HASH)) ? 1 : 0;
+        return kBinOcc4Table[tf][birth_death ? 1 : 0][segregation & 3];
+    }
+    return ilp == 1 ? bin_stepper_kernel_ilp(birth_death, segregation, bin_k, c32, flags)
+                    : bin_table_entry(birth_death, segregation, bin_k, c32, flags);
 }
 
 int bin_stepper_block(uint32_t bin_k) { return bin_k > 64 ? kBinWideBlock : kStepperBlock; }

@@ -114,7 +114,9 @@ hipError_t launch_stepper(const StepperArgs& a, int birth_death, int segregation
 // neither is set. bin_stepper_block = the variant's workgroup size.
 // ilp: 1 = the max-ILP instruction schedule of the same kernels (a second compile of ssa_kernels.hip,
 // ECDNA_ILP_BUILD): fewer stalls for lone waves, more VGPRs (3 waves per SIMD); the ABI takes it when a
-// chunk has at most one wave of replicates per SIMD.
+// chunk has at most one wave of replicates per SIMD. ilp = 2: for K = 64 / u16, the
+// default schedule capped at 128 VGPRs (4 workgroups per CU instead of 3), taken when lanes run many
+// replicates each; other K / counter widths fall back to the default schedule.
 const void* bin_stepper_kernel(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags, int ilp);
 const void* bin_stepper_kernel_ilp(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags);
 int bin_stepper_block(uint32_t bin_k);

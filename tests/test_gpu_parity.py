@@ -174,12 +174,13 @@ def test_gpu_extreme_rates_match_oracle(flags, engine_mod, oracle_mod):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("sched", ["0", "1"])
+@pytest.mark.parametrize("sched", ["0", "1", "3"])
 @pytest.mark.parametrize("name", sorted(BIN_CASES))
 def test_gpu_bin_store_both_schedules_match_oracle(name, sched, engine_mod, oracle_mod, monkeypatch):
-    """The bin stepper's two instruction schedules (ECDNA_SSA_SCHED: 0 = occupancy-first, the large-run
+    """The bin stepper's instruction schedules (ECDNA_SSA_SCHED: 0 = occupancy-first, the large-run
     default; 1 = max-ILP, taken automatically for at most one wave of replicates per SIMD, i.e. for every
-    case here) are the same kernels: both bit for bit against the oracle."""
+    case here; 3 = the 128-VGPR build of the K = 64 / u16 kernel, taken automatically at four or more
+    replicates per lane, the default elsewhere) are the same kernels: each bit for bit against the oracle."""
     monkeypatch.setenv("ECDNA_SSA_SCHED", sched)
     spec = BIN_CASES[name]
     _compare(engine_mod.run(spec, want_rows=True), oracle_mod.run(spec, mode="philox", want_rows=True), name)
@@ -219,7 +220,7 @@ def test_gpu_nminus_fast_forward_matches_oracle(name, engine_mod, oracle_mod, mo
     on N--dominated runs, under both instruction schedules. (The pure-birth case has no fast-forward.)"""
     spec = FF_SPECS[name]
     cpu = oracle_mod.run(spec, mode="philox", want_rows=True)
-    for sched in ("1", "0"):
+    for sched in ("1", "0", "3"):
         monkeypatch.setenv("ECDNA_SSA_SCHED", sched)
         _compare(engine_mod.run(spec, want_rows=True), cpu, f"{name}/sched{sched}")
     s = cpu.summaries

@@ -51,17 +51,19 @@ CASES = rotation_cases()
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("sched", ["2", "3"])  # 3: the 128-VGPR K = 64 / u16 build (the default elsewhere)
 @pytest.mark.parametrize("blocks,tick", [(8, 0), (8, 3), (1, 2)])
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_gpu_rotation_matches_oracle(name, blocks, tick, engine_mod, oracle_mod, monkeypatch):
+def test_gpu_rotation_matches_oracle(name, blocks, tick, sched, engine_mod, oracle_mod, monkeypatch):
     spec = CASES[name]
+    monkeypatch.setenv("ECDNA_SSA_SCHED", sched)
     monkeypatch.setenv("ECDNA_SSA_ROTATE", "1")
     monkeypatch.setenv("ECDNA_SSA_ROT_TICK", str(tick))
     monkeypatch.setenv("ECDNA_SSA_ROT_PARK_MIN", "1")
     monkeypatch.setenv("ECDNA_SSA_MAX_BLOCKS", str(blocks))
     gpu = engine_mod.run(spec, want_rows=True)
     cpu = oracle_mod.run(spec, mode="philox", want_rows=True)
-    _compare(gpu, cpu, f"{name}/blocks{blocks}/tick{tick}")
+    _compare(gpu, cpu, f"{name}/blocks{blocks}/tick{tick}/sched{sched}")
 
 
 @pytest.mark.gpu
@@ -73,11 +75,12 @@ def test_gpu_rotation_on_off_identical_at_scale(kmax, engine_mod, monkeypatch):
                        bin_kmax=kmax, flags=H | B)
     monkeypatch.setenv("ECDNA_SSA_MAX_BLOCKS", "512")
     runs = {}
-    for mode, tick in (("2", "11"), ("2", "6"), ("0", "11")):
+    for mode, tick, sched in (("2", "11", "2"), ("2", "6", "2"), ("2", "11", "3"), ("0", "11", "2")):
         monkeypatch.setenv("ECDNA_SSA_ROTATE", mode)
         monkeypatch.setenv("ECDNA_SSA_ROT_TICK", tick)
-        runs[(mode, tick)] = engine_mod.run(spec)
-    ref = runs[("0", "11")]
+        monkeypatch.setenv("ECDNA_SSA_SCHED", sched)  # 3: the 128-VGPR build at K = 64
+        runs[(mode, tick, sched)] = engine_mod.run(spec)
+    ref = runs[("0", "11", "2")]
     for key, r in runs.items():
         for f in ref.summaries.dtype.names:
             a, b = r.summaries[f], ref.summaries[f]
