@@ -443,10 +443,22 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
         // (auto only without f32 time and the event hash: that variant spills 12 B at 128 VGPRs)
         const bool k64u16 = c->bin_k == 64 && !c->bin_c32;
         const bool tf0 = (p->flags & (ECDNA_FLAG_TIME_F32 | ECDNA_FLAG_EVENT_HASH)) == 0;
+        // Where the max-ILP build keeps the default's occupancy (LDS bounds both: K = 64 / u32 at two
+        // workgroups per CU, K = 256; K = 64 / u16 at three) it is taken too: its schedule then costs no
+        // lanes (C5 whole, K = 64 / u32: 35.3 -> 34.1 s same-box).
+        int occ_def = 0, occ_ilp = 0;
+        CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &occ_def, ecdna::bin_stepper_kernel(p->process, p->segregation, c->bin_k, c->bin_c32, p->flags, 0),
+            (int)c->stepper_block, 0));
+        CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &occ_ilp, ecdna::bin_stepper_kernel(p->process, p->segregation, c->bin_k, c->bin_c32, p->flags, 1),
+            (int)c->stepper_block, 0));
         if (sched == 1 || (sched == 2 && max_chunk <= (uint64_t)c->cus * 256u))
             c->bin_ilp = 1;
         else if (k64u16 && (sched == 3 || (sched == 2 && tf0 && max_chunk >= 4ull * c->cus * 4u * ecdna::kStepperBlock)))
             c->bin_ilp = 2;
+        else if (sched == 2 && occ_ilp >= occ_def)
+            c->bin_ilp = 1;
         else
             c->bin_ilp = 0;
         // bin store: LDS-resident events, bounded by issue and LDS latency: every resident block helps
