@@ -483,9 +483,13 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
 
     // Replicate rotation (bin store, 256-lane blocks): on when lanes have at least three
     // replicates each (ECDNA_SSA_ROTATE = 0 off, 1 on whenever possible, 2 auto); with two (C4 8-GPU shard)
-    // the drain control is faster (74 ms against 84). Results do not depend on it. Byte offsets into
-    // bags/park are u32 in the kernel: chunks stay below 2 GiB of either.
+    // the drain control is faster (74 ms against 84). Auto also leaves it off when the caller gave a cost
+    // hint: the costliest-first start order then already balances the lanes, and parking only mixes the
+    // order up again (C4 whole sweep, same box: 710-718 ms without rotation against 738-750 with it under
+    // the 128-VGPR build, 747-749 against 792-805 under the default one). Results do not depend on it.
+    // Byte offsets into bags/park are u32 in the kernel: chunks stay below 2 GiB of either.
     const uint64_t rot_mode = env_u64("ECDNA_SSA_ROTATE", 2);
+    const bool hinted = c->d_order != nullptr;
     c->rot_tick_log2 = (uint32_t)std::min<uint64_t>(env_u64("ECDNA_SSA_ROT_TICK", 10), 30);
     bool any_rot = false;
     for (auto& ch : c->chunks) {
@@ -493,7 +497,7 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
         const uint64_t lanes = std::max<uint64_t>(1, std::min<uint64_t>(need, c->stepper_blocks_cap)) * c->stepper_block;
         const bool ok = c->bin_k && c->stepper_block == ecdna::kStepperBlock &&
                         (uint64_t)ch.n * std::max<uint64_t>(bag_bytes, ecdna::kParkVecs * 16u) < (1ull << 31);
-        if (!ok || rot_mode == 0 || (rot_mode == 2 && ch.n < 3 * lanes)) continue;
+        if (!ok || rot_mode == 0 || (rot_mode == 2 && (ch.n < 3 * lanes || hinted))) continue;
         const uint32_t per = (ch.n + ecdna::kRotParts - 1) / ecdna::kRotParts;
         ch.rot_n_pad = (per + ecdna::kRotBlock - 1) / ecdna::kRotBlock * ecdna::kRotBlock;
         ch.rot_init.assign(ecdna::kRotParts, ecdna::RotPart{});
