@@ -141,13 +141,49 @@ def algorithmic_bytes(words, n_reps: int, init_cells: int = 1) -> int:
             + n_reps * (2 * init_cells + B_SUMMARY))
 
 
+# the sources that decide the stepper's instruction stream: a committed PMC summary describes THIS build only
+# when its recorded digest of them matches (tools/pmc_summary.py stamps it)
+KERNEL_SOURCES = ("ecdna-evo_amd/csrc/ssa_kernels.hip", "ecdna-evo_amd/csrc/ssa_device.hpp",
+                  "ecdna-evo_amd/csrc/ssa_launch.h", "ecdna-evo_amd/csrc/ssa_logtab.h",
+                  "ecdna-evo_amd/csrc/ssa_api.cpp", "ecdna-evo_amd/Makefile")
+
+
+def kernel_sources_digest() -> str:
+    import hashlib
+
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(REPO, rel), "rb") as f:
+            h.update(rel.encode() + b"\0" + f.read() + b"\0")
+    return h.hexdigest()
+
+
 def load_pmc(store: str):
-    """The committed rocprofv3 PMC summary of the stepper on this workload (profiles/pmc_c3[_bins].json)."""
+    """The committed rocprofv3 PMC summary of the stepper on this workload (profiles/pmc_c3[_bins].json),
+    or {} when it was measured on other kernel sources than the ones built here (its counters would not
+    describe this build)."""
     try:
         with open(os.path.join(REPO, "profiles", "pmc_c3_bins.json" if store == "bins" else "pmc_c3.json")) as f:
-            return json.load(f)
+            pmc = json.load(f)
     except Exception:
         return {}
+    if pmc.get("kernel_sources_sha256") != kernel_sources_digest():
+        return {"stale": True, "round": pmc.get("round"), "git_head": pmc.get("git_head")}
+    return pmc
+
+
+def usable_cores() -> int:
+    """Host cores this process may use, as rayon's default pool counts them (the reference's replicate
+    loop, src/main.rs:221-224): the CPU affinity set, capped by a cgroup v2 CPU quota if one is set."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except Exception:
+        pass
+    return max(1, n)
 
 
 def rmw_ceiling():
@@ -302,6 +338,11 @@ def main():
     tot_host = tot_sets.reshape(n_sets, 16).sum(axis=0)
     assert int(tot_host[0]) == total, f"all-reduced totals count {int(tot_host[0])} replicates, expected {total}"
     assert int(tot_host[1]) == events_per_step
+    stop_reasons = {abi.STOP_NAMES[i]: int(tot_host[9 + i]) for i in range(6)}
+    errors = int(tot_host[15])
+    # the workloads are sized so that no replicate hits a capacity (cell_cap, C5's big_cap) or overflow error:
+    # a replicate cut short by one would make the events/s line count a different process
+    assert errors == 0, f"{errors} replicates stopped with an error (stop reasons {stop_reasons})"
 
     if rank == 0 and args.dump_hist:
         import numpy as np
@@ -310,12 +351,12 @@ def main():
     if rank == 0:
         avg_kernel_s = sum(kernel_ms) / len(kernel_ms) * 1e-3
         achieved = local_alg / avg_kernel_s / 1e9
-        pmc = load_pmc(args.store)
+        pmc = load_pmc(args.store) if weak else {}  # (the committed PMC summaries are C3's)
         traffic = pmc.get("hbm_bytes_per_launch")
         kernel_eps = local_events / avg_kernel_s
         transactions = None
         issue = None
-        if args.store == "bins" and weak and "valu_insts_per_event" in pmc:  # (the PMC summary is C3's)
+        if args.store == "bins" and "valu_insts_per_event" in pmc:
             per_event = pmc["valu_insts_per_event"]
             two, four = valu_measured_ceilings()
             issue = {
@@ -332,7 +373,7 @@ def main():
                         "wave64 instruction, which only the VOP2 logic/add/mov class reaches on gfx950 — most of "
                         "the stepper's instructions are in the measured 4-cycle class (tools/valu_probe.hip)",
             }
-        if args.store == "rows" and weak and "read_requests_per_event" in pmc:
+        if args.store == "rows" and "read_requests_per_event" in pmc:
             per_event = pmc["read_requests_per_event"] + pmc["write_requests_per_event"]
             ceiling = rmw_ceiling()
             transactions = {
@@ -346,7 +387,8 @@ def main():
             }
         cpu = None
         if n_gpus == 1 and not args.no_cpu_baseline:
-            threads = int(os.environ.get("ECDNA_BENCH_CPU_THREADS", "0")) or min(16, os.cpu_count() or 1)
+            # every usable core, as the reference's rayon pool (src/main.rs:221-224)
+            threads = int(os.environ.get("ECDNA_BENCH_CPU_THREADS", "0")) or usable_cores()
             cpu = cpu_baseline(threads, args.workload)
         chunk, lanes = ctx.geometry()
         line = {
@@ -370,6 +412,8 @@ def main():
                 "replicates_per_gpu": reps,
                 "replicates_total": total,
                 "events_per_step": events_per_step,
+                "stop_reasons": stop_reasons,
+                "replicate_errors": errors,
                 "parallelism": f"replicas{n_gpus} ({'contiguous' if weak else 'interleaved'} replicate-id shards, "
                                f"1 RCCL all-reduce of the histogram)",
                 "grid_lanes": lanes,
@@ -378,12 +422,23 @@ def main():
                 "kernel_events_per_s_per_gpu": kernel_eps,
             },
             "roofline": {
-                "bound": "hbm",
+                # what binds the stepper: vector-instruction issue for the bin store (its events stay in LDS
+                # and registers), HBM request rate for the row store; achieved / peak / frac below are the
+                # contract's nominal HBM view (SURVEY.md §8d algorithmic bytes of the reference's u16-row
+                # representation over the kernel's duration, vs 8 TB/s), which neither store is bound by
+                "bound": "valu_issue" if args.store == "bins" else "hbm_requests",
+                "issue_frac": issue["frac"] if issue else None,
+                "frac_kind": "nominal_hbm_algorithmic_bytes",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "pmc_source": None if not pmc else (
+                    f"stale ({pmc.get('round')}): the committed PMC summary was measured on other kernel "
+                    f"sources; counter fields omitted" if pmc.get("stale") else
+                    f"profiles/pmc_c3{'_bins' if args.store == 'bins' else ''}.json, round {pmc.get('round')}, "
+                    f"git {pmc.get('git_head')}, kernel sources match this build"),
                 "hbm_requests": transactions,
                 "valu_issue": issue,
             },

@@ -488,8 +488,18 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
     // order up again (C4 whole sweep, same box: 710-718 ms without rotation against 738-750 with it under
     // the 128-VGPR build, 747-749 against 792-805 under the default one). Results do not depend on it.
     // Byte offsets into bags/park are u32 in the kernel: chunks stay below 2 GiB of either.
-    const uint64_t rot_mode = env_u64("ECDNA_SSA_ROTATE", 2);
+    uint64_t rot_mode = env_u64("ECDNA_SSA_ROTATE", 2);
     const bool hinted = c->d_order != nullptr;
+    // Rotation hands a parked replicate only to lanes of the same partition, partition = XCC id mod
+    // kRotParts, and relies on those lanes sharing one L2 (the parked state is read with L1-bypassing
+    // loads). That holds when the agent has at most kRotParts XCCs (gfx950 SPX: 8, CPX: 1); otherwise
+    // two L2s would share a partition, so rotation stays off.
+    {
+        int xccs = 0;
+        if (hipDeviceGetAttribute(&xccs, hipDeviceAttributeNumberOfXccs, c->device) != hipSuccess || xccs < 1 ||
+            xccs > (int)ecdna::kRotParts)
+            rot_mode = 0;
+    }
     c->rot_tick_log2 = (uint32_t)std::min<uint64_t>(env_u64("ECDNA_SSA_ROT_TICK", 10), 30);
     bool any_rot = false;
     for (auto& ch : c->chunks) {

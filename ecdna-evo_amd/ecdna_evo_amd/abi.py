@@ -176,13 +176,16 @@ class RunSpec:
     big_cap: int = 0  # FLAG_BIN_STORE: large-k row capacity (cells with k > bin_kmax); 0 = cell_cap
     _keep: list = field(default_factory=list, repr=False)
 
+    def stride(self) -> int:
+        """The id step as the C ABI reads it: replicate_stride 0 means 1 (include/ecdna_ssa.h)."""
+        return self.replicate_stride if self.replicate_stride else 1
+
     def replicate_ids(self) -> np.ndarray:
         """Global ids of the call's replicates, in summary order."""
-        return self.first_replicate + np.arange(self.n_replicates, dtype=np.uint64) * np.uint64(
-            max(1, self.replicate_stride))
+        return self.first_replicate + np.arange(self.n_replicates, dtype=np.uint64) * np.uint64(self.stride())
 
     def last_replicate(self) -> int:
-        return self.first_replicate + max(0, self.n_replicates - 1) * max(1, self.replicate_stride)
+        return self.first_replicate + max(0, self.n_replicates - 1) * self.stride()
 
     def resolved_max_time(self) -> float:
         if self.max_time is not None:
@@ -204,6 +207,16 @@ class RunSpec:
         return np.asarray(cells, dtype=np.uint16), nminus
 
     def params(self) -> Params:
+        # ctypes silently masks values that do not fit a field (a stride of 2^32 would become 0, i.e. 1):
+        # reject them here instead
+        for name, bits in (("replicate_stride", 32), ("big_cap", 32), ("bin_kmax", 32), ("hist_bins", 32),
+                           ("n_replicates", 64), ("first_replicate", 64), ("seed", 64), ("max_cells", 64),
+                           ("max_iter", 64)):
+            v = getattr(self, name)
+            if not (0 <= int(v) < (1 << bits)):
+                raise ValueError(f"{name} = {v} does not fit the ABI's u{bits} field")
+        if self.cell_cap is not None and not (0 <= int(self.cell_cap) < (1 << 32)):
+            raise ValueError(f"cell_cap = {self.cell_cap} does not fit the ABI's u32 field")
         self._keep = []
         rates = np.asarray(self.rates, dtype=np.float32).reshape(-1, 4)
         n_sets = rates.shape[0]

@@ -22,7 +22,7 @@ std::map<uint32_t, uint64_t> Distribution::histogram() const {
     return h;
 }
 
-Distribution Distribution::from_histogram(const std::map<uint32_t, uint64_t>& h) {
+Distribution Distribution::from_histogram(const std::map<uint32_t, uint64_t>& h, uint64_t max_nplus) {
     // the engine counts cells in u32 (include/ecdna_ssa.h: initial N- and N+ below 2^32); checked before
     // anything is expanded, so a corrupt count fails here instead of in a terabyte allocation
     uint64_t cells = 0;
@@ -31,6 +31,8 @@ Distribution Distribution::from_histogram(const std::map<uint32_t, uint64_t>& h)
         if (kv.first != 0) cells += kv.second;
     }
     if (cells > 0xffffffffull) throw IoError("more than 2^32 - 1 N+ cells");
+    if (cells > max_nplus)
+        throw IoError(std::to_string(cells) + " N+ cells exceed the capacity " + std::to_string(max_nplus));
     Distribution d;
     d.nplus.reserve(cells);
     for (const auto& kv : h) {
@@ -74,14 +76,14 @@ uint64_t parse_uint(const std::string& t, size_t& i) {
 
 }  // namespace
 
-Distribution from_json(const std::string& t) {
+Distribution from_json(const std::string& t, uint64_t max_nplus) {
     std::map<uint32_t, uint64_t> h;
     size_t i = 0;
     skip_ws(t, i);
     if (i >= t.size() || t[i] != '{') throw IoError("expected '{'");
     ++i;
     skip_ws(t, i);
-    if (i < t.size() && t[i] == '}') return Distribution::from_histogram(h);
+    if (i < t.size() && t[i] == '}') return Distribution::from_histogram(h, max_nplus);
     for (;;) {
         skip_ws(t, i);
         if (i >= t.size() || t[i] != '"') throw IoError("expected a quoted copy number");
@@ -105,16 +107,16 @@ Distribution from_json(const std::string& t) {
         if (i < t.size() && t[i] == '}') break;
         throw IoError("expected ',' or '}'");
     }
-    return Distribution::from_histogram(h);
+    return Distribution::from_histogram(h, max_nplus);
 }
 
-Distribution load_json(const std::string& path) {
+Distribution load_json(const std::string& path, uint64_t max_nplus) {
     std::ifstream f(path);
     if (!f) throw IoError("cannot open " + path);
     std::stringstream ss;
     ss << f.rdbuf();
     try {
-        return from_json(ss.str());
+        return from_json(ss.str(), max_nplus);
     } catch (const IoError& e) {
         throw IoError("cannot load the ecDNA distribution from " + path + ": " + e.what());
     }

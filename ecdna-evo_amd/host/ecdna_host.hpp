@@ -23,8 +23,9 @@ struct Distribution {
     uint64_t cells() const { return nminus + nplus.size(); }
     std::map<uint32_t, uint64_t> histogram() const;  // {k: cells}, key 0 = n-
     // EcDNADistribution::new from a histogram; N+ cells pushed in ascending k (the reference iterates a
-    // HashMap, whose order is random per process — SURVEY.md App. B.5).
-    static Distribution from_histogram(const std::map<uint32_t, uint64_t>& h);
+    // HashMap, whose order is random per process — SURVEY.md App. B.5). More than max_nplus N+ cells
+    // throw before anything is reserved or expanded (a corrupt count cannot force a huge allocation).
+    static Distribution from_histogram(const std::map<uint32_t, uint64_t>& h, uint64_t max_nplus = 0xffffffffull);
 };
 
 struct IoError : std::runtime_error {
@@ -33,8 +34,9 @@ struct IoError : std::runtime_error {
 
 // {"0":n-,"k":cells,...} with ascending keys (dynamics.md:8).
 std::string to_json(const Distribution& d);
-Distribution from_json(const std::string& text);
-Distribution load_json(const std::string& path);  // EcDNADistribution::load
+// max_nplus: the caller's capacity for N+ cells (checked before the cells are expanded)
+Distribution from_json(const std::string& text, uint64_t max_nplus = 0xffffffffull);
+Distribution load_json(const std::string& path, uint64_t max_nplus = 0xffffffffull);  // EcDNADistribution::load
 
 // f32 `Display` of Rust (shortest round-trip, fixed notation) with '.' -> "dot" (src/lib.rs:27-45).
 std::string rate_str(float r);

@@ -62,8 +62,7 @@ int ecdna_host_save(const char* dir, const char* filename, float time, const uin
 // EcDNADistribution::load: returns the number of N+ cells (<= cap) or -1.
 int64_t ecdna_host_load(const char* path, uint16_t* out_nplus, uint64_t cap, uint64_t* out_nminus) {
     try {
-        ecdna::host::Distribution d = ecdna::host::load_json(path);
-        if (d.nplus.size() > cap) return -1;
+        ecdna::host::Distribution d = ecdna::host::load_json(path, cap);  // rejects > cap before expanding
         if (!d.nplus.empty()) std::memcpy(out_nplus, d.nplus.data(), d.nplus.size() * sizeof(uint16_t));
         *out_nminus = d.nminus;
         return (int64_t)d.nplus.size();

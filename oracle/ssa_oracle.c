@@ -697,6 +697,9 @@ static int validate(const ecdna_ssa_params_t* p, uint64_t row_stride, int want_r
     if (p->segregation < 0 || p->segregation > 3) return ECDNA_E_INVALID;
     if (p->max_iter > 0xffffffffull) return ECDNA_E_INVALID;
     const uint64_t stride = p->replicate_stride ? p->replicate_stride : 1u;
+    if (p->n_replicates > 0xffffffffull) return ECDNA_E_INVALID; /* as ssa_api.cpp validate() */
+    if (p->n_replicates && (p->n_replicates - 1) > (~0ull - p->first_replicate) / stride)
+        return ECDNA_E_INVALID; /* first + (n - 1) * stride would wrap u64 */
     if (p->n_replicates && (p->first_replicate + (p->n_replicates - 1) * stride) / p->reps_per_set >= p->n_param_sets)
         return ECDNA_E_INVALID;
     if (!p->init_copies && (p->init_nplus || p->init_set_offsets)) return ECDNA_E_INVALID;

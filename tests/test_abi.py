@@ -164,3 +164,22 @@ def test_oracle_rejects_invalid_rates(oracle_mod):
         with pytest.raises(ValueError):
             oracle_mod.run(abi.RunSpec(rates=(r,), n_replicates=2, max_cells=10))
     oracle_mod.run(abi.RunSpec(rates=((0, 3.0e38, 0, 1e-45),), n_replicates=2, max_cells=10))
+
+
+def test_runspec_rejects_values_ctypes_would_mask():
+    """ctypes silently truncates integers to the field width: a replicate_stride of 2^32 would reach C as 0
+    (= 1, contiguous ids) while RunSpec.replicate_ids() kept the wide stride."""
+    for kw in (dict(replicate_stride=1 << 32), dict(big_cap=1 << 32), dict(replicate_stride=-1),
+               dict(cell_cap=1 << 32), dict(n_replicates=-1)):
+        with pytest.raises(ValueError):
+            abi.RunSpec(**kw).params()
+    s = abi.RunSpec(n_replicates=3, first_replicate=5, replicate_stride=0)
+    assert s.replicate_ids().tolist() == [5, 6, 7] and s.last_replicate() == 7  # stride 0 reads as 1, as in C
+
+
+def test_oracle_rejects_wrapping_replicate_ids(oracle_mod):
+    """first + (n - 1) * stride wrapping u64 is invalid in the oracle as in the engine (ssa_api.cpp validate)."""
+    spec = abi.RunSpec(n_replicates=3, first_replicate=(1 << 64) - 2 ** 32, replicate_stride=(1 << 32) - 1,
+                       reps_per_set=(1 << 64) - 1, max_cells=10)
+    with pytest.raises(ValueError):
+        oracle_mod.run(spec)

@@ -149,6 +149,7 @@ def test_save_and_load_roundtrip(host, tmp_path):
     ('{"65536": 1}', -1),                       # copy number beyond u16
     ('{"1": 2,}', -1), ('{"1" 2}', -1), ('["1", 2]', -1), ("", -1),
     ('{"1": 17}', -1),                          # more N+ cells than the caller's buffer (cap 16)
+    ('{"1": 4000000000, "2": 1}', -1),          # rejected before 4e9 cells are expanded (8 GB)
 ])
 def test_load_rejects_malformed(host, tmp_path, body, want):
     p = tmp_path / "d.json"

@@ -9,6 +9,7 @@ STORE=${2:-bins}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/prof_$TAG
 mkdir -p $O
+python3 -c "import sys; sys.argv=['x']; import runpy; g=runpy.run_path('bench.py', run_name='bench_digest'); print(g['kernel_sources_digest']())" > $O/kernel_sources_sha256.txt
 timeout -k 10 400 python3 bench.py --steps 3 --warmup 1 --store $STORE > $O/bench.json 2> $O/bench.err
 echo "bench done" 
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/kt -o kt -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --store $STORE > $O/kt.log 2>&1

@@ -44,8 +44,21 @@ def main(src, tag):
                          LDS_Block_Size=int(r["LDS_Block_Size"]), Grid_Size=int(r["Grid_Size"]))
     ev = bench["config"]["events_per_step"]
     st = pmc[kname]
+    # which build the counters describe: bench.py reads the counter fields only while this digest matches
+    # the kernel sources it runs (bench.kernel_sources_digest; gpu_profile.sh records it on the box)
+    digest_path = os.path.join(src, "kernel_sources_sha256.txt")
+    digest = open(digest_path).read().strip() if os.path.exists(digest_path) else None
+    try:
+        import subprocess
+
+        head = subprocess.run(["git", "-C", REPO, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                              text=True).stdout.strip() or None
+    except Exception:
+        head = None
     out = {
         "round": tag,
+        "git_head": head,
+        "kernel_sources_sha256": digest,
         "workload": bench["config"]["workload"],
         "store": bench.get("store", "rows"),
         "kernel": kname,
