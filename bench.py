@@ -186,6 +186,16 @@ def usable_cores() -> int:
     return max(1, n)
 
 
+def cores_basis() -> str:
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota = f.read().strip()
+    except Exception:
+        quota = "n/a"
+    return f"usable cores = min(CPU affinity set {aff}, cgroup v2 cpu.max '{quota}'); os.cpu_count() {os.cpu_count()}"
+
+
 def rmw_ceiling():
     """Random 2-B read-modify-write pairs/s the chip sustains (tools/rmw_shapes.hip, 4 GiB buffer,
     best lane count; profiles/r01d_access_microbench.jsonl)."""
@@ -226,7 +236,7 @@ def cpu_baseline(threads: int, workload: str = "c3"):
     ev_ph, dt_ph = sample(n_ph, "philox")
     what = "C3 shape, replicates 0..{0} of 2^20".format(n - 1) if workload == "c3" else \
         f"{workload.upper()} shape, {n} of its {total} replicates"
-    return {"value": ev / dt, "unit": "events/s", "cores": threads, "kind": "port",
+    return {"value": ev / dt, "unit": "events/s", "cores": threads, "kind": "port", "cores_basis": cores_basis(),
             "sample": f"{what} ({ev} events, {dt:.1f} s wall), "
                       f"oracle compat mode (ChaCha8 streams seed*10+i, first-reaction, BTPE), "
                       f"{threads} threads",

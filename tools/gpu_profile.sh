@@ -20,6 +20,8 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $O/pmc_wr
 echo "pmc write done"
 timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES -T --output-format csv -d $O/pmc_sq -o pmc -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --store $STORE > $O/pmc_sq.log 2>&1
 echo "pmc sq done"
+if [ -x tools/bin/pmc_calib ]; then  # (the access-shape calibration, profiles/r01*_pmc_calibration.json)
 timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $O/calib_fetch -o pmc -- tools/bin/pmc_calib > $O/calib_fetch.log 2>&1
 timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $O/calib_write -o pmc -- tools/bin/pmc_calib > $O/calib_write.log 2>&1
 echo "calib done"
+fi
