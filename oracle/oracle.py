@@ -82,6 +82,10 @@ def lib():
     L.oracle_compat_exp1.restype = C.c_double
     L.oracle_compat_binomial.argtypes = [C.c_void_p, C.c_uint64, C.c_double]
     L.oracle_compat_binomial.restype = C.c_uint64
+    L.oracle_compat_log.argtypes = [C.c_double]
+    L.oracle_compat_log.restype = C.c_double
+    L.oracle_compat_exp.argtypes = [C.c_double]
+    L.oracle_compat_exp.restype = C.c_double
     _lib = L
     return L
 
@@ -214,6 +218,14 @@ class ChaCha:
 
     def binomial(self, n: int, p: float) -> int:
         return lib().oracle_compat_binomial(self.h, n, p)
+
+
+def compat_log(x: float) -> float:
+    return lib().oracle_compat_log(x)
+
+
+def compat_exp(x: float) -> float:
+    return lib().oracle_compat_exp(x)
 
 
 def chacha_block(state, rounds: int):

@@ -167,22 +167,143 @@ static inline double float_1_2(uint64_t bits) {
     return x.d;
 }
 
-/* Exp1 ziggurat tables: 256 layers, R = 7.69711747013104972, V = (R+1) e^-R. */
-#define ZIG_EXP_R 7.697117470131487
-static double zig_x[257], zig_f[257];
-static int zig_ready = 0;
+/* ---- correctly rounded log / exp.
+ * The reference reaches glibc's log and exp through Rust's f64::ln / f64::exp (rand_distr's ziggurat tail and
+ * wedge, BTPE). glibc rounds those to within 0.52 ulp, not always correctly, and a GPU has no glibc, so the
+ * compat mapping defines log and exp as the CORRECTLY ROUNDED functions, computed in double-double
+ * (~2^-97 relative) from basic IEEE operations and explicit fma in a fixed order; the GPU compat stepper
+ * (ecdna-evo_amd/csrc/compat_math.hpp) restates the same operations, so both agree bit for bit, and both
+ * agree with glibc wherever glibc rounds correctly (tests/test_compat_math.py). */
+#include "compat_tables.h"
 
-static void zig_init(void) {
-    if (zig_ready) return;
-    const double R = ZIG_EXP_R;
-    const double V = (R + 1.0) * exp(-R);
-    zig_x[0] = V / exp(-R);
-    zig_x[1] = R;
-    for (int i = 1; i < 256; ++i) zig_x[i + 1] = -log(exp(-zig_x[i]) + V / zig_x[i]);
-    zig_x[256] = 0.0;
-    for (int i = 0; i < 257; ++i) zig_f[i] = exp(-zig_x[i]);
-    zig_f[256] = 1.0;
-    __atomic_store_n(&zig_ready, 1, __ATOMIC_RELEASE);
+typedef struct {
+    double hi, lo;
+} dd_t;
+
+static inline dd_t dd_two_sum(double a, double b) {
+    const double s = a + b, bb = s - a;
+    dd_t r = {s, (a - (s - bb)) + (b - bb)};
+    return r;
+}
+static inline dd_t dd_fast(double a, double b) { /* |a| >= |b| or a == 0 */
+    const double s = a + b;
+    dd_t r = {s, b - (s - a)};
+    return r;
+}
+static inline dd_t dd_add(dd_t a, dd_t b) {
+    dd_t s = dd_two_sum(a.hi, b.hi);
+    const double e = s.lo + (a.lo + b.lo);
+    return dd_fast(s.hi, e);
+}
+static inline dd_t dd_mul(dd_t a, dd_t b) {
+    const double p = a.hi * b.hi;
+    const double e = fma(a.hi, b.hi, -p) + (a.hi * b.lo + a.lo * b.hi);
+    return dd_fast(p, e);
+}
+static inline dd_t dd_d(double a) {
+    dd_t r = {a, 0.0};
+    return r;
+}
+static inline dd_t dd_c(double h, double l) {
+    dd_t r = {h, l};
+    return r;
+}
+
+static const double CLOG_TAB[3 * ECDNA_CLOG_N] = ECDNA_CLOG_INIT;
+static const double CEXP_TAB[2 * 64] = ECDNA_CEXP_INIT;
+static const double ZIG_EXP_X[257] = ECDNA_ZIG_EXP_X_INIT;
+static const double ZIG_EXP_F[257] = ECDNA_ZIG_EXP_F_INIT;
+
+static inline uint64_t d2u(double x) {
+    uint64_t u;
+    memcpy(&u, &x, sizeof(u));
+    return u;
+}
+static inline double u2d(uint64_t u) {
+    double x;
+    memcpy(&x, &u, sizeof(x));
+    return x;
+}
+
+/* ln x, correctly rounded (to ~2^-97 before the final rounding). x = f 2^e, f in [181.5/256, 181.5/128);
+ * j = round(128 f), c = RN(128/j) (c = 1 for j = 128, so no cancellation near ln 1 = 0); r = f c - 1 exactly
+ * as a double-double; ln x = e ln2 + (-ln c) + log1p(r), |r| <= 0.0055, log1p by its series: terms 14..7
+ * in double, 6..1 in double-double. */
+double oracle_compat_log(double x) {
+    if (!(x > 0.0)) return x == 0.0 ? -INFINITY : NAN;
+    if (x == INFINITY) return x;
+    int64_t e = 0;
+    uint64_t u = d2u(x);
+    if ((u >> 52) == 0) { /* subnormal */
+        x = x * 0x1p54;
+        u = d2u(x);
+        e = -54;
+    }
+    e += (int64_t)(u >> 52) - 1023;
+    double f = u2d((u & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
+    if (f >= 1.41796875) { /* 181.5 / 128 */
+        f = f * 0.5;
+        e += 1;
+    }
+    const int j = (int)(f * 128.0 + 0.5); /* exact product; 91..181 */
+    const double* t = CLOG_TAB + 3 * (j - ECDNA_CLOG_J0);
+    const double c = t[0];
+    const double ph = f * c, pl = fma(f, c, -ph);
+    const dd_t r = dd_two_sum(ph - 1.0, pl); /* ph - 1 exact (ph in [0.99, 1.01]) */
+    double q = -1.0 / 14.0;
+    q = fma(r.hi, q, 1.0 / 13.0);
+    q = fma(r.hi, q, -1.0 / 12.0);
+    q = fma(r.hi, q, 1.0 / 11.0);
+    q = fma(r.hi, q, -1.0 / 10.0);
+    q = fma(r.hi, q, 1.0 / 9.0);
+    q = fma(r.hi, q, -1.0 / 8.0);
+    q = fma(r.hi, q, 1.0 / 7.0);
+    dd_t P = dd_d(q);
+    P = dd_add(dd_c(-ECDNA_CINV6_HI, -ECDNA_CINV6_LO), dd_mul(r, P));
+    P = dd_add(dd_c(ECDNA_CINV5_HI, ECDNA_CINV5_LO), dd_mul(r, P));
+    P = dd_add(dd_d(-0.25), dd_mul(r, P));
+    P = dd_add(dd_c(ECDNA_CINV3_HI, ECDNA_CINV3_LO), dd_mul(r, P));
+    P = dd_add(dd_d(-0.5), dd_mul(r, P));
+    P = dd_add(dd_d(1.0), dd_mul(r, P));
+    const dd_t l1p = dd_mul(r, P);
+    const double ed = (double)e;
+    const double eh = ed * ECDNA_CLN2_HI;
+    const dd_t eln2 = dd_fast(eh, fma(ed, ECDNA_CLN2_HI, -eh) + ed * ECDNA_CLN2_LO);
+    dd_t s = dd_add(eln2, dd_c(t[1], t[2]));
+    s = dd_add(s, l1p);
+    return s.hi + s.lo;
+}
+
+/* e^y, correctly rounded (~2^-97) for |y| <= 22 (the compat mapping needs [-R, 0], R = 7.7 the ziggurat's
+ * base; beyond 22 the reduction below is no longer exact: still deterministic, no longer guaranteed correct). k = rint(64 y / ln2), y = k ln2/64 + r with r as a double-double (the head of ln2/64 has 42 bits:
+ * k * head exact), |r| <= 0.0055; e^y = 2^(k div 64) 2^((k mod 64)/64) e^r, e^r = 1 + r P(r) with the
+ * series terms 11..7 in double, 6..1 in double-double. */
+double oracle_compat_exp(double y) {
+    if (y != y) return y;
+    if (y > 709.0) return INFINITY;
+    if (y < -745.0) return 0.0;
+    const double kd = rint(y * ECDNA_CEXP_INV_L);
+    const int64_t k = (int64_t)kd;
+    const double rh = y - kd * ECDNA_CEXP_L_HI; /* exact */
+    const double pl = kd * ECDNA_CEXP_L_LO, ple = fma(kd, ECDNA_CEXP_L_LO, -pl);
+    dd_t r = dd_two_sum(rh, -pl);
+    r = dd_fast(r.hi, r.lo - ple);
+    double q = 1.0 / 39916800.0; /* 1/11! */
+    q = fma(r.hi, q, 1.0 / 3628800.0);
+    q = fma(r.hi, q, 1.0 / 362880.0);
+    q = fma(r.hi, q, 1.0 / 40320.0);
+    q = fma(r.hi, q, 1.0 / 5040.0);
+    dd_t P = dd_d(q);
+    P = dd_add(dd_c(ECDNA_CFACT6_HI, ECDNA_CFACT6_LO), dd_mul(r, P));
+    P = dd_add(dd_c(ECDNA_CFACT5_HI, ECDNA_CFACT5_LO), dd_mul(r, P));
+    P = dd_add(dd_c(ECDNA_CFACT4_HI, ECDNA_CFACT4_LO), dd_mul(r, P));
+    P = dd_add(dd_c(ECDNA_CFACT3_HI, ECDNA_CFACT3_LO), dd_mul(r, P));
+    P = dd_add(dd_d(0.5), dd_mul(r, P));
+    P = dd_add(dd_d(1.0), dd_mul(r, P));
+    const dd_t er = dd_add(dd_d(1.0), dd_mul(r, P)); /* e^r */
+    const int64_t jj = k & 63, qq = (k - jj) / 64;
+    const dd_t v = dd_mul(dd_c(CEXP_TAB[2 * jj], CEXP_TAB[2 * jj + 1]), er);
+    return ldexp(v.hi + v.lo, (int)qq);
 }
 
 static double exp1(oracle_chacha* r) {
@@ -190,18 +311,21 @@ static double exp1(oracle_chacha* r) {
         uint64_t bits = cc_u64(r);
         int i = (int)(bits & 0xff);
         double u = float_1_2(bits) - (1.0 - 0x1p-53);
-        double x = u * zig_x[i];
-        if (x < zig_x[i + 1]) return x;
-        if (i == 0) return ZIG_EXP_R - log(gen_f64(r));
-        if (zig_f[i + 1] + (zig_f[i] - zig_f[i + 1]) * gen_f64(r) < exp(-x)) return x;
+        double x = u * ZIG_EXP_X[i];
+        if (x < ZIG_EXP_X[i + 1]) return x;
+        if (i == 0) return ECDNA_ZIG_EXP_R - oracle_compat_log(gen_f64(r));
+        if (ZIG_EXP_F[i + 1] + (ZIG_EXP_F[i] - ZIG_EXP_F[i + 1]) * gen_f64(r) < oracle_compat_exp(-x)) return x;
     }
 }
-double oracle_compat_exp1(oracle_chacha* r) {
-    zig_init();
-    return exp1(r);
-}
+double oracle_compat_exp1(oracle_chacha* r) { return exp1(r); }
 
-static inline int64_t f64_to_i64(double x) { return (int64_t)x; }
+/* Rust's `f as i64`: saturating, NaN -> 0 (a C cast of an out-of-range double is undefined) */
+static inline int64_t f64_to_i64(double x) {
+    if (x != x) return 0;
+    if (x >= 0x1p63) return INT64_MAX;
+    if (x < -0x1p63) return INT64_MIN;
+    return (int64_t)x;
+}
 
 static double stirling(double a) {
     double a2 = a * a;
@@ -272,11 +396,11 @@ static uint64_t binomial(oracle_chacha* rg, uint64_t n_u, double p_in) {
                 if (v > 1.) continue;
                 y = f64_to_i64(x);
             } else if (!(u > p3)) {
-                y = f64_to_i64(x_l + log(v) / lambda_l);
+                y = f64_to_i64(x_l + oracle_compat_log(v) / lambda_l);
                 if (y < 0) continue;
                 v *= (u - p2) * lambda_l;
             } else {
-                y = f64_to_i64(x_r - log(v) / lambda_r);
+                y = f64_to_i64(x_r - oracle_compat_log(v) / lambda_r);
                 if (y > 0 && (uint64_t)y > n_u) continue;
                 v *= (u - p3) * lambda_r;
             }
@@ -304,15 +428,15 @@ static uint64_t binomial(oracle_chacha* rg, uint64_t n_u, double p_in) {
             double kf = (double)k;
             double rho = (kf / npq) * ((kf * (kf / 3. + 0.625) + 1. / 6.) / npq + 0.5);
             double t = -0.5 * kf * kf / npq;
-            double alpha = log(v);
+            double alpha = oracle_compat_log(v);
             if (alpha < t - rho) break;
             if (alpha > t + rho) continue;
             double x1 = (double)(y + 1);
             double f1 = (double)(m + 1);
             double z = (double)(f64_to_i64(n) + 1 - m);
             double w = (double)(f64_to_i64(n) - y + 1);
-            if (alpha > x_m * log(f1 / x1) + (n - (double)m + 0.5) * log(z / w) +
-                            (double)(y - m) * log(w * p / (x1 * q)) + stirling(f1) + stirling(z) -
+            if (alpha > x_m * oracle_compat_log(f1 / x1) + (n - (double)m + 0.5) * oracle_compat_log(z / w) +
+                            (double)(y - m) * oracle_compat_log(w * p / (x1 * q)) + stirling(f1) + stirling(z) -
                             stirling(x1) - stirling(w))
                 continue;
             break;
@@ -336,7 +460,6 @@ void oracle_snapshot_check(const ecdna_ssa_params_t* p, uint32_t* sj, uint64_t n
 void oracle_compat_simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16_t* row,
                                       ecdna_rep_summary_t* out, ecdna_snapshot_t* snap_meta, uint16_t* snap_rows,
                                       uint64_t snap_stride) {
-    zig_init();
     uint32_t sj = 0;
     const uint64_t set = rid / p->reps_per_set;
     const ecdna_rates_t rt = p->rates[set];

@@ -91,6 +91,9 @@ uint64_t oracle_chacha_next_u64(oracle_chacha* r);
 uint64_t oracle_compat_gen_range(oracle_chacha* r, uint64_t n);   /* rand 0.8.5 gen_range(0..n) */
 double oracle_compat_exp1(oracle_chacha* r);                        /* rand_distr Exp1 (ziggurat) */
 uint64_t oracle_compat_binomial(oracle_chacha* r, uint64_t n, double p); /* rand_distr Binomial */
+/* The compat mapping's ln and exp: correctly rounded (double-double), DESIGN.md §4.1. */
+double oracle_compat_log(double x);
+double oracle_compat_exp(double x);
 
 #ifdef __cplusplus
 }
