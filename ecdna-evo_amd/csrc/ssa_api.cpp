@@ -83,6 +83,8 @@ int validate(const ecdna_ssa_params_t* p) {
     if (p->n_replicates && (p->first_replicate + (p->n_replicates - 1) * stride) / p->reps_per_set >= p->n_param_sets)
         return fail(ECDNA_E_INVALID, "replicate ids map past the last parameter set");
     if (p->cell_cap == 0) return fail(ECDNA_E_INVALID, "cell_cap must be >= 1");
+    if ((p->flags & ECDNA_FLAG_REFERENCE_DRAWS) && (p->flags & ECDNA_FLAG_BIN_STORE))
+        return fail(ECDNA_E_INVALID, "ECDNA_FLAG_REFERENCE_DRAWS runs the row store only (no ECDNA_FLAG_BIN_STORE)");
     if ((p->flags & ECDNA_FLAG_BIN_STORE) && p->bin_kmax != 0 && p->bin_kmax != 32 && p->bin_kmax != 64 &&
         p->bin_kmax != 256)
         return fail(ECDNA_E_INVALID, "bin_kmax must be 0 (= 64), 32, 64 or 256");
@@ -109,6 +111,45 @@ int validate(const ecdna_ssa_params_t* p) {
     }
     return ECDNA_OK;
 }
+
+// Reference draws (ECDNA_FLAG_REFERENCE_DRAWS): rand_core 0.6.4 seed_from_u64 — the 32-byte ChaCha key filled
+// by a PCG32 sequence from the seed (little-endian words).
+void chacha_key_from_u64(uint64_t state, uint32_t key[8]) {
+    const uint64_t mul = 6364136223846793005ull, inc = 11634580027462260723ull;
+    for (int i = 0; i < 8; ++i) {
+        state = state * mul + inc;
+        const uint32_t xorshifted = (uint32_t)(((state >> 18) ^ state) >> 27);
+        const uint32_t rot = (uint32_t)(state >> 59);
+        key[i] = (xorshifted >> rot) | (xorshifted << ((32u - rot) & 31u));
+    }
+}
+
+// rand_distr 0.4.3 BTPE setup of Binomial(n, 1/2) (the step-0 constants; oracle/ssa_compat.c computes the same
+// per call), one row of refdraws::kBtpeRow doubles per copy number k = n / 2: npq, m, p1, x_m, x_l, x_r, c,
+// p2, lambda_l, lambda_r, p3, p4. Only n >= 20 (n p >= 10) takes BTPE.
+void btpe_setup(uint64_t n_u, double* row) {
+    const double p = 0.5, q = 1.0 - p;
+    const double n = (double)n_u;
+    const double np = n * p;
+    const double npq = np * q;
+    const double f_m = np + p;
+    const int64_t m = (int64_t)f_m;
+    const double p1 = std::floor(2.195 * std::sqrt(npq) - 4.6 * q) + 0.5;
+    const double x_m = (double)m + 0.5;
+    const double x_l = x_m - p1;
+    const double x_r = x_m + p1;
+    const double c = 0.134 + 20.5 / (15.3 + (double)m);
+    const double p2 = p1 * (1. + 2. * c);
+    const double al = (f_m - x_l) / (f_m - x_l * p);
+    const double lambda_l = al * (1. + 0.5 * al);
+    const double ar = (x_r - f_m) / (x_r * q);
+    const double lambda_r = ar * (1. + 0.5 * ar);
+    const double p3 = p2 + c / lambda_l;
+    const double p4 = p3 + c / lambda_r;
+    const double v[12] = {npq, (double)m, p1, x_m, x_l, x_r, c, p2, lambda_l, lambda_r, p3, p4};
+    for (int i = 0; i < 12; ++i) row[i] = v[i];
+}
+constexpr int kBtpeRow = 16;  // refdraws::kBtpeRow
 
 struct Chunk {
     uint64_t first;  // local index of the first replicate
@@ -138,6 +179,10 @@ struct ecdna_ssa_ctx {
     int bin_ilp = 0;  // the bin stepper's schedule: 0 default, 1 max-ILP (lone waves), 2 128-VGPR K = 64 (ssa_launch.h)
     void* d_bags = nullptr;
     uint32_t stepper_block = ecdna::kStepperBlock;
+    // reference draws (ECDNA_FLAG_REFERENCE_DRAWS): the ChaCha8 key and the BTPE constants per copy number
+    bool refdraws = false;
+    uint32_t* d_ref_key = nullptr;
+    double* d_ref_btpe = nullptr;
     // owned copies of the host inputs
     std::vector<ecdna_rates_t> rates;
     std::vector<uint16_t> init_copies;
@@ -219,12 +264,33 @@ void free_ctx(ecdna_ssa_ctx* c) {
     (void)hipFree(c->d_rot_parts);
     (void)hipFree(c->d_rot_flags);
     (void)hipFree(c->d_rot_park);
+    (void)hipFree(c->d_ref_key);
+    (void)hipFree(c->d_ref_btpe);
     (void)hipFree(c->d_hist_own);
     (void)hipFree(c->d_tot_own);
     delete c;
 }
 
 }  // namespace
+
+// library-internal entry points for ssa_comm.cpp (the RCCL reduction)
+__attribute__((visibility("hidden"))) int ecdna_ssa_internal_fail(int code, const std::string& msg) {
+    return fail(code, msg);
+}
+
+__attribute__((visibility("hidden"))) int ecdna_ssa_internal_ctx_outputs(ecdna_ssa_ctx* c, uint64_t** d_hist,
+                                                                         ecdna_totals_t** d_tot, uint32_t* n_sets,
+                                                                         uint32_t* bins, int* device, void** stream) {
+    if (!c) return fail(ECDNA_E_INVALID, "ctx is NULL");
+    if (!c->launched) return fail(ECDNA_E_STATE, "reduce before launch");
+    *d_hist = c->d_hist;
+    *d_tot = c->d_tot;
+    *n_sets = c->p.n_param_sets;
+    *bins = c->p.hist_bins;
+    *device = c->device;
+    *stream = c->last_stream;
+    return ECDNA_OK;
+}
 
 extern "C" {
 
@@ -238,6 +304,7 @@ const char* ecdna_ssa_strerror(int code) {
         case ECDNA_E_NOMEM: return "device out of memory";
         case ECDNA_E_NODEVICE: return "no usable gfx950 device";
         case ECDNA_E_STATE: return "invalid call order";
+        case ECDNA_E_COMM: return "RCCL communication error (or librccl.so.1 missing)";
         default: return "unknown error";
     }
 }
@@ -428,7 +495,20 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
     // persistent stepper grid: as many resident lanes as the occupancy allows
     c->window = env_u64("ECDNA_SSA_WINDOW", 1) ? 1 : 0;
     int per_cu = 0;
-    if (c->bin_k) {
+    c->refdraws = (p->flags & ECDNA_FLAG_REFERENCE_DRAWS) != 0;
+    if (c->refdraws) {
+        uint32_t key[8];
+        chacha_key_from_u64(p->seed, key);
+        CTX_TRY(hipMalloc(&c->d_ref_key, sizeof(key)));
+        CTX_TRY(hipMemcpy(c->d_ref_key, key, sizeof(key), hipMemcpyHostToDevice));
+        std::vector<double> bt((uint64_t)32768 * kBtpeRow, 0.0);
+        for (uint64_t k = 10; k < 32768; ++k) btpe_setup(2 * k, bt.data() + k * kBtpeRow);
+        CTX_TRY(hipMalloc(&c->d_ref_btpe, bt.size() * sizeof(double)));
+        CTX_TRY(hipMemcpy(c->d_ref_btpe, bt.data(), bt.size() * sizeof(double), hipMemcpyHostToDevice));
+        c->stepper_block = (uint32_t)ecdna::refdraws_block();
+        CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, ecdna::refdraws_kernel(p->process, p->segregation), (int)c->stepper_block, 0));
+    } else if (c->bin_k) {
         // Instruction schedule: with at most one wave of replicates per SIMD (every chunk within 256 lanes
         // per CU) each wave runs alone and waits on its own dependencies, and the max-ILP schedule is faster
         // (C2 8.6 -> 8.1 ms, C5 8-GPU shard 22.0 -> 21.1 s); with more, issue binds and the default schedule
@@ -623,8 +703,12 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
                                    hipMemcpyHostToDevice, st));
         }
 
+        a.ref_key = c->d_ref_key;
+        a.ref_btpe = c->d_ref_btpe;
         HIP_TRY(hipEventRecord(ch.ev[0], st));
-        if (c->bin_k)
+        if (c->refdraws)
+            HIP_TRY(ecdna::launch_refdraws(a, p.process, p.segregation, blocks, st));
+        else if (c->bin_k)
             HIP_TRY(ecdna::launch_bin_stepper(a, p.process, p.segregation, c->bin_k, c->bin_c32, c->bin_ilp, blocks, st));
         else
             HIP_TRY(ecdna::launch_stepper(a, p.process, p.segregation, c->window, blocks, st));

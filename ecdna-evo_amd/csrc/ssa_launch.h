@@ -72,6 +72,10 @@ struct StepperArgs {
     uint32_t rot_n_pad;             // replicates per partition, multiple of kRotBlock
     uint32_t rot_tick_log2;
     int32_t rot_park_min;           // park at a tick only if at least this many replicates wait
+    // reference draws (ECDNA_FLAG_REFERENCE_DRAWS, ssa_refdraws.hip): the ChaCha8 key of seed_from_u64(seed)
+    // (8 words) and the BTPE constants of Binomial(2k, 1/2) per copy number k (refdraws::kBtpeRow doubles)
+    const uint32_t* ref_key;
+    const double* ref_btpe;
 };
 
 // Histogram / totals pass over one chunk.
@@ -123,5 +127,10 @@ int bin_stepper_block(uint32_t bin_k);
 hipError_t launch_bin_stepper(const StepperArgs& a, int birth_death, int segregation, uint32_t bin_k, int c32, int ilp,
                               uint32_t blocks, hipStream_t stream);
 hipError_t launch_hist(const HistArgs& a, uint32_t blocks, hipStream_t stream);
+// The reference-draws stepper (row store; ssa_refdraws.hip)
+const void* refdraws_kernel(int birth_death, int segregation);
+int refdraws_block();
+hipError_t launch_refdraws(const StepperArgs& a, int birth_death, int segregation, uint32_t blocks,
+                           hipStream_t stream);
 
 }  // namespace ecdna

@@ -1,0 +1,231 @@
+// ssa_refdraws.hip — the SSA stepper under the reference's own draw structure (ECDNA_FLAG_REFERENCE_DRAWS;
+// DESIGN.md §4.1): a correctness path that reproduces, per replicate, the sequence of random draws the Rust
+// reference makes, so a GPU run can be compared seed for seed with the reference semantics
+// (oracle/ssa_compat.c restates the same on the CPU and the parity tests require bit-identical results).
+//
+// One replicate per lane, cells in a u16 row in HBM in swap_remove order (the row store; the bin store's
+// canonical order is a different arrangement, so it has no seed-for-seed counterpart in the reference). Per
+// event, in the reference's order:
+//   * sosa 3.0.3 loop (call sites src/main.rs:92-99, 166-173; reconstructed): stop checks
+//     (iterations, cells, f32 time), then the FIRST-REACTION method over update_state's population vector
+//     [n-, n+(, n-, n+)] (src/process.rs:187-196, 339-344) with f32 rates (src/main.rs:67, 139): channel i
+//     draws tau_i = Exp(rate_i * pop_i) unless its propensity is 0 (no draw), the first minimum wins;
+//   * advance_step (src/process.rs:147-184, 291-336): ProliferateNPlus picks a uniform N+ cell with
+//     gen_range + swap_remove (ecdna-lib), segregates 2k copies with rand_distr's Binomial(2k, 1/2) under the
+//     CLI's Segregation rule (src/segregation.rs:110-194) and pushes the daughters
+//     (src/proliferation.rs:25-111); DeathNPlus removes a uniform cell (src/proliferation.rs:125-133); the N-
+//     events count (src/proliferation.rs:113-117, 135-139);
+//   * process.time += tau in f32 (src/process.rs:184, 336).
+// RNG: ChaCha8Rng::seed_from_u64(seed) on stream seed * 10 + r (src/main.rs:56-58), refdraws.hpp.
+#include "refdraws.hpp"
+#include "ssa_launch.h"
+
+#pragma clang fp contract(off)
+
+namespace ecdna {
+
+namespace {
+__constant__ const double kZigX[257] = ECDNA_ZIG_EXP_X_INIT;
+__constant__ const double kZigF[257] = ECDNA_ZIG_EXP_F_INIT;
+__constant__ const double kCLog[3 * ECDNA_CLOG_N] = ECDNA_CLOG_INIT;
+__constant__ const double kCExp[128] = ECDNA_CEXP_INIT;
+constexpr uint64_t kFnv0 = 0xcbf29ce484222325ull;
+constexpr uint64_t kFnvP = 0x100000001b3ull;
+constexpr uint32_t kRefBlock = 256;
+}  // namespace
+
+template <bool BD, int SEG>
+__global__ void __launch_bounds__(kRefBlock) ssa_stepper_refdraws(const StepperArgs a) {
+    __shared__ uint32_t ccbuf[16 * kRefBlock];
+    __shared__ double zx[257], zf[257], clog[3 * ECDNA_CLOG_N], cexp[128];
+    // the sampler tables, staged in LDS (per-lane divergent indices)
+    for (uint32_t i = threadIdx.x; i < 257u; i += blockDim.x) {
+        zx[i] = kZigX[i];
+        zf[i] = kZigF[i];
+    }
+    for (uint32_t i = threadIdx.x; i < 3u * ECDNA_CLOG_N; i += blockDim.x) clog[i] = kCLog[i];
+    for (uint32_t i = threadIdx.x; i < 128u; i += blockDim.x) cexp[i] = kCExp[i];
+    __syncthreads();
+    const uint32_t tid = threadIdx.x;
+    const bool hash_on = (a.flags & ECDNA_FLAG_EVENT_HASH) != 0;
+    constexpr int K = BD ? 4 : 2;
+
+    refdraws::ChaCha8 rng;
+    rng.key = a.ref_key;
+    rng.buf = ccbuf + tid;
+    rng.stride = kRefBlock;
+
+    for (;;) {
+        uint32_t li = atomicAdd(a.head, 1u);
+        if (li >= a.n) break;
+        const uint64_t rid = a.rid0 + (uint64_t)li * a.rid_stride;
+        uint16_t* row = a.rows + (uint64_t)li * a.row_stride;
+        const uint64_t set = rid / a.reps_per_set;
+        const float4 r4 = a.rates[set];
+        const float rates[4] = {r4.x, r4.y, r4.z, r4.w};
+        const uint16_t* src = a.init_copies;
+        uint32_t np = a.init_nplus;
+        if (a.init_offsets) {
+            src = a.init_copies + a.init_offsets[set];
+            np = a.init_offsets[set + 1] - a.init_offsets[set];
+        }
+        for (uint32_t j = 0; j < np; ++j) row[j] = src[j];
+        uint32_t nm = (uint32_t)(a.init_nminus_set ? a.init_nminus_set[set] : a.init_nminus);
+        const uint64_t stream = a.seed * 10ull + rid;  // src/main.rs:56-58
+        rng.counter = 0;
+        rng.s_lo = (uint32_t)stream;
+        rng.s_hi = (uint32_t)(stream >> 32);
+        rng.pos = 16;
+
+        uint64_t h = kFnv0;
+        float t = 0.0f;
+        uint32_t e = 0, stop = 0, err = 0, sj = 0;
+        uint32_t cnt[4] = {0u, 0u, 0u, 0u};
+        uint32_t uneven_n = 0;
+        if (np == 0 && nm == 0) {  // ensure!(!distribution.is_empty()) src/process.rs:88, 232
+            err = ECDNA_REP_ERR_EMPTY;
+            stop = ECDNA_STOP_ERROR;
+        }
+        while (!stop) {
+            if (e >= a.max_iter) {
+                stop = ECDNA_STOP_MAX_ITER;
+                break;
+            }
+            if ((uint64_t)nm + np >= a.stop_cells) {
+                stop = ECDNA_STOP_MAX_CELLS;
+                break;
+            }
+            if (t >= a.max_time32) {
+                stop = ECDNA_STOP_MAX_TIME;
+                break;
+            }
+            // first-reaction method, channel order [PN-, PN+, DN-, DN+]
+            const uint32_t pop[4] = {nm, np, nm, np};
+            int ch = -1;
+            float best = __builtin_inff();
+#pragma unroll
+            for (int c = 0; c < K; ++c) {
+                const float lambda = rates[c] * (float)pop[c];
+                if (!(lambda > 0.0f)) continue;
+                const float inv = 1.0f / lambda;
+                const float tau = (float)refdraws::exp1(rng, zx, zf, clog, cexp) * inv;
+                if (ch < 0 || tau < best) {
+                    best = tau;
+                    ch = c;
+                }
+            }
+            if (ch < 0) {
+                stop = ECDNA_STOP_ABSORBING;
+                break;
+            }
+            if (a.n_snap) {  // advance_step's snapshot rule (src/process.rs:122-145), before the event
+                const uint64_t total = (uint64_t)nm + np;
+                while (sj < a.n_snap) {
+                    bool any = false;
+                    for (uint32_t q = sj; q < a.n_snap; ++q) any |= a.snap_cells[q] == total;
+                    if (!any) break;
+                    ecdna_snapshot_t* m = a.snap_meta + (uint64_t)li * a.n_snap + sj;
+                    m->time = (double)t;
+                    m->nminus = nm;
+                    m->nplus = np;
+                    m->taken = 1u;
+                    m->reserved = 0u;
+                    if (a.snap_rows) {
+                        uint16_t* dst = a.snap_rows + ((uint64_t)li * a.n_snap + sj) * a.snap_stride;
+                        for (uint32_t j = 0; j < np; ++j) dst[j] = row[j];
+                    }
+                    ++sj;
+                }
+            }
+            uint64_t x = (uint64_t)ch;
+            if (ch == ECDNA_EV_PROLIF_NMINUS) {
+                nm += 1;
+            } else if (ch == ECDNA_EV_DEATH_NMINUS) {
+                nm -= 1;
+            } else if (ch == ECDNA_EV_DEATH_NPLUS) {
+                const uint32_t i = (uint32_t)rng.gen_range(np);
+                row[i] = row[np - 1];
+                np -= 1;
+                x |= (uint64_t)i << 20;
+            } else {  // ProliferateNPlus
+                const uint32_t i = (uint32_t)rng.gen_range(np);
+                const uint32_t k = row[i];
+                if (k > 32767u) {  // checked_mul panic (src/proliferation.rs:63-67)
+                    err = ECDNA_REP_ERR_OVERFLOW;
+                    stop = ECDNA_STOP_ERROR;
+                    break;
+                }
+                const uint32_t n = 2u * k;
+                uint32_t k1 = 0;
+                int un = 0;  // 0 False, 1 True, 2 TrueWithoutNMinusIncrease
+                if (SEG == ECDNA_SEG_DETERMINISTIC) {
+                    k1 = n / 2u;
+                } else if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN) {
+                    int tries = 0;
+                    do {
+                        k1 = refdraws::binomial_half(rng, n, a.ref_btpe, clog);
+                    } while ((k1 == 0u || k1 == n) && ++tries < 4096);
+                    if (k1 == 0u || k1 == n) {
+                        err = ECDNA_REP_ERR_REJECTION;
+                        stop = ECDNA_STOP_ERROR;
+                        break;
+                    }
+                } else {
+                    k1 = refdraws::binomial_half(rng, n, a.ref_btpe, clog);
+                    if (k1 == 0u || k1 == n) un = SEG == ECDNA_SEG_BINOMIAL_NO_NMINUS ? 2 : 1;
+                }
+                if (un == 0 && np + 1u > a.cell_cap) {
+                    err = ECDNA_REP_ERR_CELL_CAP;
+                    stop = ECDNA_STOP_ERROR;
+                    break;
+                }
+                row[i] = row[np - 1];  // pick_remove_random_nplus: swap_remove(i)
+                np -= 1;
+                if (un == 0) {
+                    row[np++] = (uint16_t)k1;
+                    row[np++] = (uint16_t)(n - k1);
+                } else {
+                    if (un == 1) nm += 1;
+                    row[np++] = (uint16_t)n;
+                    uneven_n += 1;
+                }
+                x |= ((uint64_t)k1 << 2) | ((uint64_t)i << 20);
+            }
+            cnt[ch] += 1;
+            e += 1;
+            t = t + best;
+            if (hash_on) h = (h ^ x) * kFnvP;
+        }
+        ecdna_rep_summary_t* s = a.summaries + li;
+        s->nminus = nm;
+        s->nplus = np;
+        s->iters = e;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) s->events_by_type[c] = cnt[c];
+        s->uneven = uneven_n;
+        s->time = (double)t;
+        s->event_hash = hash_on ? h : 0ull;
+        s->stop_reason = stop;
+        s->error = err;
+    }
+}
+
+#define ECDNA_REF_SEG(BD)                                                                                    \
+    {(const void*)ssa_stepper_refdraws<BD, 0>, (const void*)ssa_stepper_refdraws<BD, 1>,                      \
+     (const void*)ssa_stepper_refdraws<BD, 2>, (const void*)ssa_stepper_refdraws<BD, 3>}
+static const void* const kRefTable[2][4] = {ECDNA_REF_SEG(false), ECDNA_REF_SEG(true)};
+
+const void* refdraws_kernel(int birth_death, int segregation) {
+    return kRefTable[birth_death ? 1 : 0][segregation & 3];
+}
+
+int refdraws_block() { return (int)kRefBlock; }
+
+hipError_t launch_refdraws(const StepperArgs& a, int birth_death, int segregation, uint32_t blocks,
+                           hipStream_t stream) {
+    StepperArgs copy = a;
+    void* args[] = {&copy};
+    return hipLaunchKernel(refdraws_kernel(birth_death, segregation), dim3(blocks), dim3(kRefBlock), args, 0, stream);
+}
+
+}  // namespace ecdna

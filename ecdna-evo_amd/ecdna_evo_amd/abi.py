@@ -14,7 +14,7 @@ from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # ecdna_process_t (ProcessType, src/clap_app.rs:311-315)
 PURE_BIRTH = 0
@@ -48,7 +48,8 @@ FLAG_EVENT_HASH = 0x4
 FLAG_SNAPSHOT_ROWS = 0x8
 
 OK = 0
-E_INVALID, E_HIP, E_NOMEM, E_NODEVICE, E_STATE = -1, -2, -3, -4, -5
+E_INVALID, E_HIP, E_NOMEM, E_NODEVICE, E_STATE, E_COMM = -1, -2, -3, -4, -5, -6
+COMM_ID_BYTES = 128
 
 MAX_ITER = 1_000_000_000  # src/main.rs:23
 MAX_CELLS = 1_000_000_000  # src/main.rs:25
@@ -95,6 +96,9 @@ STATS_DTYPE = np.dtype([("mean", "<f8"), ("entropy", "<f8"), ("frequency", "<f8"
 assert STATS_DTYPE.itemsize == 64
 FLAG_REP_STATS = 0x10
 FLAG_BIN_STORE = 0x20  # cells binned by copy number; bin_kmax = 64 or 256
+# the reference's own draw structure (ChaCha8 streams seed*10+r, first reaction, rand_distr samplers, f32 time;
+# row store only): seed for seed the oracle's compat mode
+FLAG_REFERENCE_DRAWS = 0x40
 
 
 SNAPSHOT_DTYPE = np.dtype([("time", "<f8"), ("nminus", "<u8"), ("nplus", "<u8"), ("taken", "<u4"),

@@ -38,6 +38,12 @@ EXPORTS = [
     "ecdna_ssa_ctx_row_stride",
     "ecdna_ssa_ctx_geometry",
     "ecdna_ssa_ctx_destroy",
+    "ecdna_ssa_comm_unique_id",
+    "ecdna_ssa_comm_init_rank",
+    "ecdna_ssa_comm_init_all",
+    "ecdna_ssa_comm_destroy",
+    "ecdna_ssa_reduce_hist",
+    "ecdna_ssa_ctx_reduce",
 ]
 
 
@@ -97,6 +103,18 @@ def lib():
     L.ecdna_ssa_ctx_geometry.restype = C.c_int
     L.ecdna_ssa_ctx_destroy.argtypes = [C.c_void_p]
     L.ecdna_ssa_ctx_destroy.restype = C.c_int
+    L.ecdna_ssa_comm_unique_id.argtypes = [C.c_void_p]
+    L.ecdna_ssa_comm_unique_id.restype = C.c_int
+    L.ecdna_ssa_comm_init_rank.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, P(C.c_void_p)]
+    L.ecdna_ssa_comm_init_rank.restype = C.c_int
+    L.ecdna_ssa_comm_init_all.argtypes = [C.c_int, P(C.c_int), P(C.c_void_p)]
+    L.ecdna_ssa_comm_init_all.restype = C.c_int
+    L.ecdna_ssa_comm_destroy.argtypes = [C.c_void_p]
+    L.ecdna_ssa_comm_destroy.restype = C.c_int
+    L.ecdna_ssa_reduce_hist.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
+    L.ecdna_ssa_reduce_hist.restype = C.c_int
+    L.ecdna_ssa_ctx_reduce.argtypes = [C.c_void_p, C.c_void_p]
+    L.ecdna_ssa_ctx_reduce.restype = C.c_int
     if L.ecdna_ssa_abi_version() != abi.ABI_VERSION:
         raise EngineError("ABI version mismatch between libecdna_ssa.so and ecdna_evo_amd.abi")
     _lib = L
@@ -112,6 +130,39 @@ def _check(rc: int, what: str):
 
 def device_count() -> int:
     return lib().ecdna_ssa_device_count()
+
+
+class Comm:
+    """An RCCL communicator made by the engine's C ABI (ecdna_ssa_comm_init_all / init_rank): the multi-GPU
+    reduction of ecdna_ssa_ctx_reduce."""
+
+    def __init__(self, handle):
+        self.h = handle
+
+    @staticmethod
+    def init_all(devices) -> list:
+        devs = (C.c_int * len(devices))(*devices)
+        out = (C.c_void_p * len(devices))()
+        _check(lib().ecdna_ssa_comm_init_all(len(devices), devs, out), "ecdna_ssa_comm_init_all")
+        return [Comm(C.c_void_p(out[i])) for i in range(len(devices))]
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * abi.COMM_ID_BYTES)()
+        _check(lib().ecdna_ssa_comm_unique_id(buf), "ecdna_ssa_comm_unique_id")
+        return bytes(buf)
+
+    @staticmethod
+    def init_rank(uid: bytes, n_ranks: int, rank: int, device: int) -> "Comm":
+        buf = (C.c_uint8 * abi.COMM_ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        _check(lib().ecdna_ssa_comm_init_rank(buf, n_ranks, rank, device, C.byref(h)), "ecdna_ssa_comm_init_rank")
+        return Comm(h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().ecdna_ssa_comm_destroy(self.h)
+            self.h = None
 
 
 class Result:
@@ -166,6 +217,10 @@ class Context:
         s, hh = C.c_float(), C.c_float()
         _check(lib().ecdna_ssa_ctx_sync(self.h, C.byref(s), C.byref(hh)), "ecdna_ssa_ctx_sync")
         return s.value, hh.value
+
+    def reduce(self, comm: "Comm"):
+        """All-reduce (sum) this context's histogram and totals over `comm` on its launch stream (RCCL)."""
+        _check(lib().ecdna_ssa_ctx_reduce(self.h, comm.h), "ecdna_ssa_ctx_reduce")
 
     def geometry(self):
         a, b = C.c_uint64(), C.c_uint64()

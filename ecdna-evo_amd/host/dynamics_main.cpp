@@ -8,14 +8,19 @@
 // Additions: --gpus N (replicate shards on N devices, one host thread each), --time {f32,f64}
 // (default f32 = the reference's process.time), --cell-cap (row capacity; needed with --years),
 // --hist-bins, --dry-run (print the resolved options as JSON and exit), --cell-store {bins,rows}
-// (default bins: copy-number counters in LDS) and --bin-kmax {64,256}.
+// (default bins: copy-number counters in LDS), --bin-kmax {64,256}, --draws
+// {philox,reference} (reference: the Rust binary's own draw structure, ChaCha8 + rand_distr, seed for seed;
+// row store) and --pooled FILE (the run's pooled copy-number histogram and totals, all-reduced over the
+// GPUs with RCCL through ecdna_ssa_ctx_reduce, written as JSON).
 #include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
 #include <ctime>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -58,6 +63,8 @@ struct Options {
     bool dry_run = false;
     bool rows = false;       // --cell-store rows
     uint32_t bin_kmax = 64;  // --bin-kmax
+    bool reference_draws = false;  // --draws reference
+    std::string pooled;            // --pooled FILE
 };
 
 [[noreturn]] void usage_error(const std::string& msg) {
@@ -96,6 +103,9 @@ void print_help() {
         "      --dry-run                    print the resolved options as JSON and exit\n"
         "      --cell-store <bins|rows>     N+ cell store of the engine [default: bins]\n"
         "      --bin-kmax <64|256>          copy numbers held as counters by the bin store [default: 64]\n"
+        "      --draws <philox|reference>   random draws: the engine's Philox mapping, or the reference's\n"
+        "                                   own (ChaCha8 + rand_distr, seed for seed; row store) [default: philox]\n"
+        "      --pooled <FILE>              write the run's pooled histogram and totals (RCCL-reduced) as JSON\n"
         "  -h, --help                       Print help\n");
 }
 
@@ -218,6 +228,12 @@ Options parse(int argc, char** argv) {
             const uint64_t v = parse_u64(a, need(a));
             if (v != 64 && v != 256) usage_error("--bin-kmax must be 64 or 256");
             o.bin_kmax = (uint32_t)v;
+        } else if (a == "--draws") {
+            const std::string v = need(a);
+            if (v != "philox" && v != "reference") usage_error("--draws must be philox or reference");
+            o.reference_draws = v == "reference";
+        } else if (a == "--pooled") {
+            o.pooled = need(a);
         } else if (!a.empty() && a[0] == '-') {
             usage_error("unexpected argument '" + a + "' found");
         } else {
@@ -233,6 +249,7 @@ Options parse(int argc, char** argv) {
         usage_error("the argument '--years <YEARS>' cannot be used with '--cells <CELLS>'");
     if (o.debug && (o.has_years || o.has_cells || o.sequential || o.has_runs || o.verbosity))
         usage_error("the argument '--debug' cannot be used with the other run options");
+    if (o.reference_draws) o.rows = true;  // the reference's draws address cells in swap_remove order
     return o;
 }
 
@@ -304,9 +321,34 @@ const char* stop_name(uint32_t s) {
     return s < 6 ? n[s] : "?";
 }
 
+// Replicate shard g of `gpus`: [runs g / gpus, runs (g + 1) / gpus) — the contiguous split of
+// ecdna_evo_amd.shard.shard_range (tests/test_host.py checks the two agree).
+void shard_of(uint64_t runs, int gpus, int g, uint64_t& first, uint64_t& n) {
+    first = runs * (uint64_t)g / (uint64_t)gpus;
+    n = runs * (uint64_t)(g + 1) / (uint64_t)gpus - first;
+}
+
+// Every shard thread reaches the reduction (an RCCL collective: all ranks must join) or none does.
+struct Rendezvous {
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0, failed = 0, total = 0;
+    bool all_ok(bool ok) {
+        std::unique_lock<std::mutex> lk(mu);
+        arrived += 1;
+        failed += ok ? 0 : 1;
+        if (arrived == total) cv.notify_all();
+        cv.wait(lk, [&] { return arrived == total; });
+        return failed == 0;
+    }
+};
+
 struct Shard {
     int device;
     uint64_t first, n;
+    void* comm = nullptr;  // RCCL communicator of this device (--pooled), or null
+    std::vector<uint64_t> hist;
+    std::vector<ecdna_totals_t> totals;
     std::vector<ecdna_rep_summary_t> summ;
     std::vector<uint16_t> rows;
     std::vector<ecdna_snapshot_t> snap_meta;
@@ -316,7 +358,7 @@ struct Shard {
     std::string err;
 };
 
-void run_shard(const ecdna_ssa_params_t& base, Shard& sh) {
+void run_shard(const ecdna_ssa_params_t& base, Shard& sh, Rendezvous* rv) {
     ecdna_ssa_params_t p = base;
     p.device = sh.device;
     p.first_replicate = sh.first;
@@ -342,6 +384,18 @@ void run_shard(const ecdna_ssa_params_t& base, Shard& sh) {
         sh.snap_rows.resize(sh.n * p.n_snapshots * st);
         sh.rc = ecdna_ssa_ctx_download_snapshots(c, sh.snap_meta.data(), sh.snap_rows.data());
     }
+    if (rv) {  // --pooled: the run's histogram and totals, all-reduced over the devices' shards (RCCL)
+        const bool ok = rv->all_ok(sh.rc == 0);
+        if (ok) {
+            sh.rc = ecdna_ssa_ctx_reduce(c, sh.comm);
+            sh.hist.resize((uint64_t)p.n_param_sets * p.hist_bins);
+            sh.totals.resize(p.n_param_sets);
+            if (!sh.rc) sh.rc = ecdna_ssa_ctx_download(c, nullptr, sh.hist.data(), sh.totals.data(), nullptr);
+        } else if (!sh.rc) {
+            sh.rc = ECDNA_E_STATE;
+            sh.err = "another device's shard failed; no reduction";
+        }
+    }
     if (sh.rc && sh.err.empty()) sh.err = ecdna_ssa_last_error_message();
     if (c) ecdna_ssa_ctx_destroy(c);
 }
@@ -362,19 +416,29 @@ int main(int argc, char** argv) {
         return 1;
     }
     const uint64_t years_cap = r.years;
+    // shards: one per GPU (sequential / debug: one; never more shards than replicates, so that every device
+    // of the reduction has a shard)
+    const int planned_gpus = (int)std::max<uint64_t>(1, std::min<uint64_t>(r.parallel ? o.gpus : 1, r.runs));
+    std::string shards_json = "[";
+    for (int g = 0; g < planned_gpus; ++g) {
+        uint64_t f, n;
+        shard_of(r.runs, planned_gpus, g, f, n);
+        shards_json += (g ? ",[" : "[") + std::to_string(f) + "," + std::to_string(n) + "]";
+    }
+    shards_json += "]";
     if (o.dry_run) {
         std::printf(
             "{\"process\":\"%s\",\"segregation\":\"%s\",\"b0\":%.9g,\"b1\":%.9g,\"d0\":%.9g,\"d1\":%.9g,\"cells\":%llu,"
             "\"years\":%llu,\"runs\":%llu,\"seed\":%llu,\"verbosity\":%d,\"parallel\":%s,\"snapshots\":%s,"
             "\"subsamples\":%s,\"initial\":%s,\"cell_cap\":%llu,\"first_idx\":%llu,\"max_iter\":%llu,"
-            "\"time\":\"%s\",\"gpus\":%d,\"cell_store\":\"%s\",\"bin_kmax\":%u}\n",
+            "\"time\":\"%s\",\"gpus\":%d,\"cell_store\":\"%s\",\"bin_kmax\":%u,\"draws\":\"%s\",\"shards\":%s}\n",
             r.birth_death ? "BirthDeath" : "PureBirth", o.segregation_name.c_str(), (double)o.b0, (double)o.b1,
             (double)r.d0, (double)r.d1, (unsigned long long)r.cells,
             (unsigned long long)years_cap, (unsigned long long)r.runs, (unsigned long long)o.seed, r.verbosity,
             r.parallel ? "true" : "false", json_list(r.snapshots).c_str(), json_list(o.subsamples).c_str(),
             ecdna::host::to_json(r.initial).c_str(), (unsigned long long)r.cell_cap,
             (unsigned long long)(o.seed * 10), (unsigned long long)kMaxIter, o.time_f64 ? "f64" : "f32", o.gpus,
-            o.rows ? "rows" : "bins", o.bin_kmax);
+            o.rows ? "rows" : "bins", o.bin_kmax, o.reference_draws ? "reference" : "philox", shards_json.c_str());
         return 0;
     }
 
@@ -396,7 +460,8 @@ int main(int argc, char** argv) {
     p.max_time = (double)(float)years_cap;  // `years as f32`, src/clap_app.rs:205
     p.max_iter = kMaxIter;
     p.cell_cap = (uint32_t)std::min<uint64_t>(r.cell_cap, 0xffffffffull);
-    p.flags = (o.time_f64 ? 0u : ECDNA_FLAG_TIME_F32) | ECDNA_FLAG_SNAPSHOT_ROWS | (o.rows ? 0u : ECDNA_FLAG_BIN_STORE);
+    p.flags = (o.time_f64 ? 0u : ECDNA_FLAG_TIME_F32) | ECDNA_FLAG_SNAPSHOT_ROWS | (o.rows ? 0u : ECDNA_FLAG_BIN_STORE) |
+              (o.reference_draws ? ECDNA_FLAG_REFERENCE_DRAWS : 0u);
     p.bin_kmax = o.rows ? 0u : o.bin_kmax;
     p.init_copies = r.initial.nplus.empty() ? nullptr : r.initial.nplus.data();
     p.init_nplus = (uint32_t)r.initial.nplus.size();
@@ -404,25 +469,37 @@ int main(int argc, char** argv) {
     p.snapshot_cells = r.snapshots.data();
     p.n_snapshots = (uint32_t)r.snapshots.size();
 
-    // shards: one per GPU (sequential / debug: one)
-    int gpus = (r.parallel ? o.gpus : 1);
     const int avail = ecdna_ssa_device_count();
     if (avail < 1) {
         std::fprintf(stderr, "error: %s\n", ecdna_ssa_strerror(ECDNA_E_NODEVICE));
         return 1;
     }
-    gpus = std::min(gpus, avail);
+    const int gpus = std::min(planned_gpus, avail);
     std::vector<Shard> shards(gpus);
     for (int g = 0; g < gpus; ++g) {
         shards[g].device = g;
-        shards[g].first = r.runs * g / gpus;
-        shards[g].n = r.runs * (g + 1) / gpus - shards[g].first;
+        shard_of(r.runs, gpus, g, shards[g].first, shards[g].n);
     }
+    Rendezvous rv;
+    rv.total = gpus;
+    std::vector<void*> comms;
+    if (!o.pooled.empty() && r.runs) {  // one RCCL communicator per device (ncclCommInitAll)
+        std::vector<int> devs(gpus);
+        for (int g = 0; g < gpus; ++g) devs[g] = g;
+        comms.assign(gpus, nullptr);
+        if (int rc = ecdna_ssa_comm_init_all(gpus, devs.data(), comms.data())) {
+            std::fprintf(stderr, "error: %s (%s)\n", ecdna_ssa_strerror(rc), ecdna_ssa_last_error_message());
+            return 1;
+        }
+        for (int g = 0; g < gpus; ++g) shards[g].comm = comms[g];
+    }
+    Rendezvous* rvp = comms.empty() ? nullptr : &rv;
     std::vector<std::thread> th;
     for (int g = 1; g < gpus; ++g)
-        if (shards[g].n) th.emplace_back(run_shard, std::cref(p), std::ref(shards[g]));
-    if (shards[0].n) run_shard(p, shards[0]);
+        if (shards[g].n) th.emplace_back(run_shard, std::cref(p), std::ref(shards[g]), rvp);
+    if (shards[0].n) run_shard(p, shards[0], rvp);
     for (auto& t : th) t.join();
+    for (void* cm : comms) ecdna_ssa_comm_destroy(cm);
     for (auto& sh : shards) {
         if (sh.rc) {
             std::fprintf(stderr, "error on device %d: %s (%s)\n", sh.device, ecdna_ssa_strerror(sh.rc),
@@ -475,6 +552,27 @@ int main(int argc, char** argv) {
     } catch (const std::exception& e) {
         std::fprintf(stderr, "error: %s\n", e.what());
         return 1;
+    }
+    if (!o.pooled.empty() && !shards.empty() && !shards[0].hist.empty()) {  // every shard holds the reduced sums
+        const ecdna_totals_t& t = shards[0].totals[0];
+        std::string js = "{\"histogram\":{";
+        bool first = true;
+        for (uint32_t b = 0; b < p.hist_bins; ++b) {
+            if (!shards[0].hist[b]) continue;
+            js += (first ? "\"" : ",\"") + std::to_string(b) + "\":" + std::to_string(shards[0].hist[b]);
+            first = false;
+        }
+        js += "},\"overflow_bin\":" + std::to_string(p.hist_bins - 1) + ",\"replicates\":" + std::to_string(t.replicates) +
+              ",\"events\":" + std::to_string(t.events) + ",\"nminus\":" + std::to_string(t.nminus) +
+              ",\"nplus\":" + std::to_string(t.nplus) + ",\"errors\":" + std::to_string(t.errors) +
+              ",\"stop_reasons\":[";
+        for (int k = 0; k < 6; ++k) js += (k ? "," : "") + std::to_string(t.stop_reasons[k]);
+        js += "],\"gpus\":" + std::to_string(gpus) + "}\n";
+        FILE* f = std::fopen(o.pooled.c_str(), "w");
+        if (!f || std::fputs(js.c_str(), f) < 0 || std::fclose(f) != 0) {
+            std::fprintf(stderr, "error: cannot write %s\n", o.pooled.c_str());
+            return 1;
+        }
     }
     std::printf("%s End simulation\n", now_str().c_str());  // src/main.rs:226
     return 0;

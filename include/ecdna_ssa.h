@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ECDNA_SSA_ABI_VERSION 5
+#define ECDNA_SSA_ABI_VERSION 6
 
 /* Process type — ProcessType (src/clap_app.rs:311-315); chosen as BirthDeath
  * when d0 > 0 or d1 > 0 (src/clap_app.rs:163-174, 194-200). */
@@ -107,6 +107,15 @@ typedef enum {
  * oracle restatement). Final and snapshot rows come back in canonical order: k = 1 cells, k = 2
  * cells, ..., k = bin_kmax cells, then the large-k row. */
 #define ECDNA_FLAG_BIN_STORE 0x20u
+/* Reference draw structure (row store only; not with ECDNA_FLAG_BIN_STORE): instead of the engine's Philox
+ * mapping, replicate r draws exactly what the Rust reference draws for replicate index r — ChaCha8Rng
+ * seed_from_u64(seed) on stream seed*10 + r (src/main.rs:56-58), the first-reaction method over f32
+ * propensities with rand_distr's Exp1 ziggurat, gen_range + swap_remove for cell picks, rand_distr's
+ * Binomial (BINV / BTPE) for segregation — and accumulates time in f32 (process.time, src/process.rs:184;
+ * ECDNA_FLAG_TIME_F32 is implied). log and exp are the correctly rounded functions (the reference's glibc
+ * calls agree with them wherever glibc rounds correctly). A correctness path for seed-for-seed comparison
+ * with the reference semantics, not a fast path. */
+#define ECDNA_FLAG_REFERENCE_DRAWS 0x40u
 
 /* API return codes. */
 #define ECDNA_OK 0
@@ -115,6 +124,7 @@ typedef enum {
 #define ECDNA_E_NOMEM (-3)     /* device allocation failed */
 #define ECDNA_E_NODEVICE (-4)  /* no usable gfx950 device */
 #define ECDNA_E_STATE (-5)     /* call order (e.g. download before launch) */
+#define ECDNA_E_COMM (-6)      /* RCCL error, or librccl.so.1 not loadable (multi-GPU reduction only) */
 
 /* Rates of one parameter set: ReactionRates([b0, b1, d0, d1]) (src/main.rs:67, 139). f32 as in Cli
  * (src/clap_app.rs:41-55). Each must be finite and >= 0 (else ECDNA_E_INVALID; the reference does not
@@ -277,6 +287,32 @@ int64_t ecdna_ssa_ctx_row_stride(const ecdna_ssa_ctx* c);
 /* Replicates per chunk (memory bound) and lanes of the persistent stepper grid. */
 int ecdna_ssa_ctx_geometry(const ecdna_ssa_ctx* c, uint64_t* chunk_replicates, uint64_t* grid_lanes);
 int ecdna_ssa_ctx_destroy(ecdna_ssa_ctx* c);
+
+/* ---- Multi-GPU reduction (ABI v6; RCCL over xGMI).
+ * Replicates shard over GPUs by GLOBAL id (first_replicate / replicate_stride), so every shard draws exactly
+ * the streams the same replicates draw in one big run, and the whole run's histogram and totals are the
+ * element-wise sum of the shards' — one all-reduce (ncclUint64, ncclSum), exact and order-independent. This
+ * replaces the reference's collection of per-replicate results from its rayon loop (src/main.rs:221-224)
+ * when the replicates live on several GPUs.
+ * A communicator is an RCCL ncclComm_t passed as void*: made here (ecdna_ssa_comm_init_all for one process
+ * driving several devices, one host thread per device; ecdna_ssa_comm_init_rank for one process per device
+ * with the unique id of ecdna_ssa_comm_unique_id shared by the caller), or made by the caller with RCCL. RCCL
+ * (librccl.so.1) is loaded at the first of these calls; without it they return ECDNA_E_COMM. */
+#define ECDNA_COMM_ID_BYTES 128
+int ecdna_ssa_comm_unique_id(uint8_t out_id[ECDNA_COMM_ID_BYTES]);
+int ecdna_ssa_comm_init_rank(const uint8_t id[ECDNA_COMM_ID_BYTES], int n_ranks, int rank, int device,
+                             void** out_comm);
+/* out_comms[n_devices]: one communicator per device of devices[] (ncclCommInitAll). */
+int ecdna_ssa_comm_init_all(int n_devices, const int* devices, void** out_comms);
+int ecdna_ssa_comm_destroy(void* comm);
+/* In-place all-reduce (sum) over `comm` of a run's DEVICE histogram [n_param_sets * hist_bins] u64 and totals
+ * [n_param_sets], enqueued on `stream` (a hipStream_t; NULL = default). Every rank of the communicator must
+ * call it with the same n_param_sets and hist_bins. Asynchronous. */
+int ecdna_ssa_reduce_hist(void* comm, uint64_t* d_hist, ecdna_totals_t* d_totals, uint32_t n_param_sets,
+                          uint32_t hist_bins, void* stream);
+/* The same on a context's current outputs (ecdna_ssa_ctx_set_outputs or its own), on the stream of its last
+ * launch; ecdna_ssa_ctx_download then returns the reduced histogram and totals. */
+int ecdna_ssa_ctx_reduce(ecdna_ssa_ctx* c, void* comm);
 
 #ifdef __cplusplus
 }

@@ -117,7 +117,9 @@ def test_invalid_parameters_rejected(product_lib):
     bad_rates = [abi.RunSpec(rates=(r,), n_replicates=4) for r in
                  ((1, float("inf"), 0, 0), (1, 1, float("nan"), 0), (1, 1, 0, -0.5), (-1e-30, 1, 0, 0))]
     bad += [r.params() for r in bad_rates]  # rates must be finite and >= 0
-    keep = [s, s2, s3, bad_rates]  # noqa: F841  (host arrays referenced by the params)
+    s4 = abi.RunSpec(n_replicates=4, flags=abi.FLAG_REFERENCE_DRAWS | abi.FLAG_BIN_STORE)
+    bad.append(s4.params())  # the reference draws run the row store only
+    keep = [s, s2, s3, s4, bad_rates]  # noqa: F841  (host arrays referenced by the params)
     for q in bad:
         h = C.c_void_p()
         rc = product_lib.ecdna_ssa_ctx_create(C.byref(q), C.byref(h))
@@ -183,3 +185,22 @@ def test_oracle_rejects_wrapping_replicate_ids(oracle_mod):
                        reps_per_set=(1 << 64) - 1, max_cells=10)
     with pytest.raises(ValueError):
         oracle_mod.run(spec)
+
+
+def test_reduce_entry_points_validate_arguments(product_lib):
+    """The RCCL reduction rejects missing communicators / buffers before touching RCCL or a device."""
+    import ctypes as C
+
+    L = product_lib
+    L.ecdna_ssa_reduce_hist.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
+    L.ecdna_ssa_ctx_reduce.argtypes = [C.c_void_p, C.c_void_p]
+    L.ecdna_ssa_comm_init_all.argtypes = [C.c_int, C.c_void_p, C.c_void_p]
+    L.ecdna_ssa_comm_init_rank.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    assert L.ecdna_ssa_reduce_hist(None, None, None, 1, 8, None) == abi.E_INVALID
+    assert L.ecdna_ssa_ctx_reduce(None, None) == abi.E_INVALID
+    assert L.ecdna_ssa_comm_init_all(0, None, None) == abi.E_INVALID
+    uid = (C.c_uint8 * abi.COMM_ID_BYTES)()
+    out = C.c_void_p()
+    assert L.ecdna_ssa_comm_init_rank(uid, 2, 5, 0, C.byref(out)) == abi.E_INVALID  # rank >= n_ranks
+    assert L.ecdna_ssa_comm_destroy(None) == 0
+    assert L.ecdna_ssa_strerror(abi.E_COMM)

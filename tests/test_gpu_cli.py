@@ -74,12 +74,14 @@ CASES = {
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("store", ["bins", "rows"])
+@pytest.mark.parametrize("store", ["bins", "rows", "reference"])
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_cli_writes_what_the_reference_writes(name, store, engine_mod, oracle_mod, tmp_path):
+    """store "reference": --draws reference, the Rust binary's own draw structure (ChaCha8 + rand_distr), so
+    every snapshot and end-of-run file equals the compat oracle's seed for seed."""
     args, c = CASES[name]
-    out = subprocess.run([CLI, *args, "--cell-store", store, str(tmp_path)], capture_output=True, text=True,
-                         timeout=300)
+    extra = ["--draws", "reference"] if store == "reference" else ["--cell-store", store]
+    out = subprocess.run([CLI, *args, *extra, str(tmp_path)], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr
     runs = int(args[args.index("--runs") + 1])
     seed = int(args[args.index("--seed") + 1])
@@ -87,9 +89,33 @@ def test_cli_writes_what_the_reference_writes(name, store, engine_mod, oracle_mo
     spec = abi.RunSpec(process=c["process"], rates=(c["rates"],), seed=seed, n_replicates=runs, max_cells=c["cells"],
                        snapshots=snaps, bin_kmax=64 if store == "bins" else 0,
                        flags=abi.FLAG_TIME_F32 | abi.FLAG_SNAPSHOT_ROWS | (abi.FLAG_BIN_STORE if store == "bins" else 0))
-    res = oracle_mod.run(spec, mode="philox", want_rows=True)
+    res = oracle_mod.run(spec, mode="compat" if store == "reference" else "philox", want_rows=True)
     want = expected_files(spec, res, c["rates"], c["subs"])
     got = written_files(tmp_path)
     assert set(got) == set(want)
     for k in want:
         assert got[k] == want[k], k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("store", ["bins", "rows"])
+def test_cli_pooled_histogram_is_the_reduced_run(store, engine_mod, tmp_path):
+    """--pooled: the run's histogram and totals all-reduced over the GPUs' shards with RCCL
+    (ecdna_ssa_comm_init_all + ecdna_ssa_ctx_reduce; one device on this box): equal to one engine run of all
+    replicates."""
+    pooled = tmp_path / "pooled.json"
+    args = ["--runs", "64", "--seed", "42", "--b1", "1.5", "--d0", "0.3", "--d1", "0.3", "-c", "900",
+            "--cell-store", store, "--pooled", str(pooled)]
+    out = subprocess.run([CLI, *args, str(tmp_path / "out")], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    got = json.load(open(pooled))
+    spec = abi.RunSpec(process=abi.BIRTH_DEATH, rates=((1, 1.5, 0.3, 0.3),), seed=42, n_replicates=64, max_cells=900,
+                       snapshots=abi.default_snapshots(900), bin_kmax=64 if store == "bins" else 0,
+                       flags=abi.FLAG_TIME_F32 | abi.FLAG_SNAPSHOT_ROWS | (abi.FLAG_BIN_STORE if store == "bins" else 0))
+    r = engine_mod.run(spec)
+    want = {str(b): int(v) for b, v in enumerate(r.hist[0]) if v}
+    assert got["histogram"] == want
+    t = r.totals[0]
+    assert (got["replicates"], got["events"], got["nminus"], got["nplus"], got["errors"]) == \
+        (64, int(t["events"]), int(t["nminus"]), int(t["nplus"]), 0)
+    assert got["stop_reasons"] == [int(x) for x in t["stop_reasons"]]

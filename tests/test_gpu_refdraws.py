@@ -1,0 +1,70 @@
+"""GPU reference-draws mode (ECDNA_FLAG_REFERENCE_DRAWS) against the CPU oracle's compat mode,
+bit for bit: ChaCha8Rng::seed_from_u64(seed) on stream seed*10 + r (src/main.rs:56-58), the first-reaction
+method over f32 propensities with rand_distr's Exp1 ziggurat, gen_range + swap_remove picks, rand_distr's
+Binomial (BINV for 2k < 20, BTPE above) and f32 process.time (src/process.rs:184, 336).
+
+Every row-store parity case of tests/cases.py runs through it (both processes, the four segregation rules,
+stop reasons and errors, snapshots, ABC sets, shards, large copy numbers up to k = 5000 through BTPE): per
+replicate summaries including the f32 time bits and the event hash, the final rows in swap_remove order,
+histograms, totals and snapshots must be identical. The oracle's compat mode is the reference's semantics as
+reconstructed from the pinned crates; its outputs are also committed
+(tests/golden/refdraws_cases.npz) and the engine must reproduce them without the oracle.
+"""
+import dataclasses
+import os
+
+import numpy as np
+import pytest
+
+from cases import cases
+from ecdna_evo_amd import abi
+from test_gpu_parity import _compare
+
+R = abi.FLAG_REFERENCE_DRAWS
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def refdraws_cases():
+    return {name: dataclasses.replace(spec, flags=spec.flags | R, _keep=[]) for name, spec in cases().items()}
+
+
+REF_CASES = refdraws_cases()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(REF_CASES))
+def test_gpu_reference_draws_match_compat_oracle(name, engine_mod, oracle_mod):
+    spec = REF_CASES[name]
+    gpu = engine_mod.run(spec, want_rows=True)
+    cpu = oracle_mod.run(spec, mode="compat", want_rows=True)
+    _compare(gpu, cpu, name)
+
+
+@pytest.mark.gpu
+def test_gpu_reference_draws_reproduce_committed_fixture(engine_mod):
+    import make_golden
+
+    fx = np.load(os.path.join(GOLDEN, "refdraws_cases.npz"))
+    for name, spec in sorted(REF_CASES.items()):
+        r = engine_mod.run(spec, want_rows=True)
+        want = fx[f"{name}__summaries"]
+        for f in want.dtype.names:
+            np.testing.assert_array_equal(r.summaries[f], want[f], err_msg=f"{name}: {f}")
+        np.testing.assert_array_equal(r.hist, fx[f"{name}__hist"], err_msg=name)
+        assert make_golden.rows_digest(r) == str(fx[f"{name}__rows_sha256"]), name
+
+
+@pytest.mark.gpu
+def test_gpu_reference_draws_c3_sample(engine_mod, oracle_mod):
+    """Replicates 0..1023 of the C3 configuration (b0 = 1, b1 = 1.5, d = 0.3 to 1e4 cells), seed 42: the
+    engine's reference-draws run equals the compat oracle replicate by replicate (hash on)."""
+    spec = abi.RunSpec(seed=42, process=abi.BIRTH_DEATH, rates=((1.0, 1.5, 0.3, 0.3),), reps_per_set=1 << 20,
+                       n_replicates=1024, max_cells=10_000, hist_bins=1025, flags=abi.FLAG_EVENT_HASH | R)
+    g = engine_mod.run(spec)
+    c = oracle_mod.run(spec, mode="compat")
+    for f in g.summaries.dtype.names:
+        a, b = g.summaries[f], c.summaries[f]
+        if f == "time":
+            a, b = a.view(np.uint64), b.view(np.uint64)
+        np.testing.assert_array_equal(a, b, err_msg=f)
+    np.testing.assert_array_equal(g.hist, c.hist)

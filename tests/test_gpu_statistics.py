@@ -259,3 +259,110 @@ def test_c3_bin_store_and_row_store_agree_in_law(engine_mod):
     ma = (np.arange(1025) * a.hist[0]).sum() / a.hist[0].sum()
     mb = (np.arange(1025) * b.hist[0]).sum() / b.hist[0].sum()
     assert abs(ma - mb) / ma < 0.01
+
+
+# ---- the north star's KS clause on the birth-death configurations (BASELINE.json configs[2..4]): the engine's
+# philox mapping, in the bench's own settings, against committed reference-semantics fixtures (ChaCha8 +
+# first-reaction + rand_distr samplers + f32 time: tests/golden/make_golden.py, oracle compat mode), and the
+# engine's reference-draws mode against the same fixtures seed for seed.
+
+
+def _fixture(name):
+    return np.load(os.path.join(GOLDEN, f"{name}_compat_seed42.npz"))
+
+
+def _per_replicate_laws(s, g, p_min):
+    """Two-sample KS on per-replicate statistics (replicates are independent; cells within one are not): final
+    N- and N+ counts, events, and the N- fraction of the surviving replicates."""
+    from scipy import stats
+
+    for f in ("nminus", "nplus", "iters"):
+        p = stats.ks_2samp(s[f].astype(np.float64), g[f].astype(np.float64)).pvalue
+        assert p > p_min, (f, p)
+    ca, cb = s["nminus"] + s["nplus"], g["nminus"].astype(np.int64) + g["nplus"]
+    fa = s["nminus"][ca > 0] / ca[ca > 0]
+    fb = g["nminus"][cb > 0] / cb[cb > 0]
+    assert stats.ks_2samp(fa, fb).pvalue > p_min
+
+
+def _ks_crit(n, m, alpha):
+    """Two-sample KS critical value (asymptotic) at level alpha for sample sizes n, m."""
+    return float(np.sqrt(-0.5 * np.log(alpha / 2.0)) * np.sqrt((n + m) / (n * m)))
+
+
+BENCH_STORES = {"bins": dict(flags=abi.FLAG_BIN_STORE), "rows": dict(flags=0)}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("store", sorted(BENCH_STORES))
+def test_c3_ks_against_reference_semantics(engine_mod, store):
+    """C3 (2^20 replicates, the metric's configuration, bench settings: f64 time, bin store K = 32 or the row
+    store) against the reference-semantics C3 fixture (65,536 replicates): pooled copy-number histogram KS
+    < 0.01 (CPU null with a second philox seed: 5e-5) and per-replicate laws."""
+    import make_golden
+
+    g = _fixture("c3")
+    kw = dict(BENCH_STORES[store], bin_kmax=32 if store == "bins" else 0)
+    r = engine_mod.run(make_golden.c3_spec(n=1 << 20, **kw))
+    _invariants(r, make_golden.c3_spec())
+    ks = _ks(r.hist[0], g["hist"][0])
+    assert ks < KS_TOL, ks
+    _per_replicate_laws(r.summaries, g, 1e-4)
+    ext_a = np.mean(r.summaries["stop_reason"] == abi.STOP_ABSORBING)
+    ext_b = np.mean(g["stop_reason"] == abi.STOP_ABSORBING)
+    assert abs(ext_a - ext_b) < 5 * np.sqrt(ext_b * (1 - ext_b) / len(g["stop_reason"]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("store", sorted(BENCH_STORES))
+def test_c4_subset_ks_against_reference_semantics(engine_mod, store):
+    """16 sets of the C4 ABC sweep spanning s in [1, 2.5], d in [0, 0.7] and k0 in {1, 16, 128} (bench settings:
+    bin store K = 64), 16,384 replicates per set against the fixture's 4,096: pooled KS < 0.01 over all sets;
+    per set, KS below the two-sample critical value at alpha = 1e-4 (replicate counts; CPU null max 0.0065)
+    and per-replicate laws."""
+    import make_golden
+
+    g = _fixture("c4_subset")
+    kw = dict(BENCH_STORES[store], bin_kmax=64 if store == "bins" else 0)
+    r = engine_mod.run(make_golden.c4_subset_spec(reps_per_set=16384, **kw))
+    gh = g["hist"].reshape(16, -1)
+    assert _ks(r.hist.sum(axis=0), gh.sum(axis=0)) < KS_TOL
+    crit = _ks_crit(16384, 4096, 1e-4)
+    for i in range(16):
+        assert _ks(r.hist[i], gh[i]) < crit, (i, make_golden.C4_SETS[i])
+        sa = r.summaries[i * 16384:(i + 1) * 16384]
+        sb = {f: g[f][i * 4096:(i + 1) * 4096] for f in ("nminus", "nplus", "iters")}
+        _per_replicate_laws(sa, sb, 1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("store", sorted(BENCH_STORES))
+def test_c5_shaped_ks_against_reference_semantics(engine_mod, store):
+    """C5's turnover process (b = 1, d = 0.9, {1: 1000}) to 2e4 cells with f32 time like the reference's
+    process.time (bench settings otherwise: bin store K = 64), 32,768 replicates against the fixture's 4,096:
+    pooled KS < 0.01 (CPU null 2e-4) and per-replicate laws."""
+    import make_golden
+
+    g = _fixture("c5_shaped")
+    kw = dict(flags=BENCH_STORES[store]["flags"] | abi.FLAG_TIME_F32, bin_kmax=64 if store == "bins" else 0)
+    r = engine_mod.run(make_golden.c5_shaped_spec(n=32768, **kw))
+    assert np.all(r.summaries["error"] == 0)
+    assert _ks(r.hist[0], g["hist"][0]) < KS_TOL
+    _per_replicate_laws(r.summaries, g, 1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["c3", "c4_subset", "c5_shaped"])
+def test_reference_draws_reproduce_bd_fixtures_seed_for_seed(engine_mod, name):
+    """ECDNA_FLAG_REFERENCE_DRAWS (the Rust reference's draw structure) on the fixtures' exact configurations
+    and replicate ids: every replicate's final n-, n+, events and stop reason, and the pooled histograms,
+    equal the reference-semantics CPU run's (the fixture) — seed for seed, not just in law."""
+    import make_golden
+
+    spec = {"c3": make_golden.c3_spec, "c4_subset": make_golden.c4_subset_spec,
+            "c5_shaped": make_golden.c5_shaped_spec}[name](flags=abi.FLAG_REFERENCE_DRAWS)
+    g = _fixture(name)
+    r = engine_mod.run(spec)
+    np.testing.assert_array_equal(r.hist.reshape(-1), g["hist"].reshape(-1))
+    for f in ("nminus", "nplus", "iters", "stop_reason"):
+        np.testing.assert_array_equal(r.summaries[f].astype(np.int64), g[f].astype(np.int64), err_msg=f)

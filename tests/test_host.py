@@ -245,3 +245,24 @@ def test_cli_cell_store_options(host):
     for bad in (["--cell-store", "tree"], ["--bin-kmax", "100"]):
         out = subprocess.run([CLI, "--dry-run", *bad, "/tmp/ecdna_out"], capture_output=True, text=True)
         assert out.returncode != 0
+
+
+@pytest.mark.parametrize("runs", [1, 2, 5, 12, 100, 1001])
+@pytest.mark.parametrize("gpus", [1, 2, 3, 8])
+def test_cli_shards_match_shard_range(host, runs, gpus):
+    """--gpus N splits the replicates exactly as ecdna_evo_amd.shard.shard_range (contiguous global ids), with
+    never more shards than replicates (every device of the RCCL reduction holds a shard)."""
+    from ecdna_evo_amd import shard
+
+    g = min(gpus, runs)
+    want = [list(shard.shard_range(r, g, runs)) for r in range(g)]
+    assert dry("--runs", str(runs), "--gpus", str(gpus))["shards"] == want
+    assert dry("--runs", str(runs), "--gpus", str(gpus), "--sequential")["shards"] == [[0, runs]]
+
+
+def test_cli_draws_option(host):
+    assert dry()["draws"] == "philox"
+    d = dry("--draws", "reference")
+    assert (d["draws"], d["cell_store"]) == ("reference", "rows")  # the reference's draws need the row store
+    out = subprocess.run([CLI, "--dry-run", "--draws", "chacha", "/tmp/ecdna_out"], capture_output=True, text=True)
+    assert out.returncode != 0

@@ -119,9 +119,10 @@ def _ks_pooled(h1, h2):
 
 
 def test_philox_and_reference_semantics_agree_in_law(oracle_mod):
-    """The engine's draw mapping vs the reference's samplers on a birth-death run: per-replicate
-    statistics (two-sample KS) and the pooled copy-number histogram."""
-    base = dict(process=abi.BIRTH_DEATH, rates=((1.0, 1.5, 0.3, 0.3),), n_replicates=6000, max_cells=300,
+    """The engine's draw mapping vs the reference's samplers on a birth-death run (C3 rates, 300 cells, 40,000
+    replicates per side): per-replicate statistics (two-sample KS) and the pooled copy-number histogram within
+    the north star's KS tolerance, 0.01 (measured: 0.0012; two philox seeds: 0.0005)."""
+    base = dict(process=abi.BIRTH_DEATH, rates=((1.0, 1.5, 0.3, 0.3),), n_replicates=40_000, max_cells=300,
                 hist_bins=257, flags=0)
     a = oracle_mod.run(abi.RunSpec(seed=1, **base), mode="philox")
     b = oracle_mod.run(abi.RunSpec(seed=2, **base), mode="compat")
@@ -130,5 +131,5 @@ def test_philox_and_reference_semantics_agree_in_law(oracle_mod):
         assert stats.ks_2samp(sa[f], sb[f]).pvalue > 1e-3, f
     ext_a = np.mean(sa["stop_reason"] == abi.STOP_ABSORBING)
     ext_b = np.mean(sb["stop_reason"] == abi.STOP_ABSORBING)
-    assert abs(ext_a - ext_b) < 0.03
-    assert _ks_pooled(a.hist[0].astype(float), b.hist[0].astype(float)) < 0.02
+    assert abs(ext_a - ext_b) < 0.015
+    assert _ks_pooled(a.hist[0].astype(float), b.hist[0].astype(float)) < 0.01
