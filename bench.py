@@ -91,9 +91,11 @@ WORKLOAD_KMAX = {"c2": 32, "c3": BENCH_BIN_KMAX, "c4": 64, "c5": 64}
 
 
 def workload_spec(first: int, n: int, total: int, seed: int = 42, device: int = 0, store: str = "bins",
-                  bin_kmax: Optional[int] = None, workload: str = "c3", stride: int = 1) -> abi.RunSpec:
+                  bin_kmax: Optional[int] = None, workload: str = "c3", stride: int = 1,
+                  max_cells: Optional[int] = None) -> abi.RunSpec:
     """Replicates first, first + stride, ... (n of them) of the workload's `total` (SURVEY.md §8d shapes);
-    bin_kmax None = the workload's default (WORKLOAD_KMAX)."""
+    bin_kmax None = the workload's default (WORKLOAD_KMAX); max_cells None = the workload's (rehearsals of
+    the multi-rank paths shrink it, tests/test_gpu_bench_dist.py)."""
     if bin_kmax is None:
         bin_kmax = WORKLOAD_KMAX[workload]
     common = dict(seed=seed, first_replicate=first, n_replicates=n, replicate_stride=stride, hist_bins=1025,
@@ -117,6 +119,8 @@ def workload_spec(first: int, n: int, total: int, seed: int = 42, device: int = 
                  max_time=1000.0, init={1: 1000}, big_cap=1 << 16 if store == "bins" else 0)
     else:
         raise ValueError(workload)
+    if max_cells is not None:
+        d["max_cells"] = max_cells
     return abi.RunSpec(segregation=abi.SEG_BINOMIAL, bin_kmax=bin_kmax if store == "bins" else 0, **common, **d)
 
 
@@ -263,6 +267,9 @@ def main():
     ap.add_argument("--dump-hist", default="", help="rank 0 saves the reduced histogram and totals (.npz)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3",
                     help="BASELINE.json config; c3 (default) is the metric's weak-scaling line")
+    ap.add_argument("--total", type=int, default=None,
+                    help="rehearsal only: replicates in total for the strong-scaling workloads (c2/c4/c5)")
+    ap.add_argument("--max-cells", type=int, default=None, help="rehearsal only: override the workload's cell cap")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -291,11 +298,11 @@ def main():
         first, n = shard.weak_range(rank, reps)
         stride = 1
     else:  # a fixed total over the ranks, interleaved ids
-        total = WORKLOADS[args.workload][0]
+        total = args.total or WORKLOADS[args.workload][0]
         first, n, stride = shard.interleaved_range(rank, n_gpus, total)
         reps = n
     spec = workload_spec(first, n, total, device=local if distributed else 0, store=args.store,
-                         bin_kmax=args.bin_kmax, workload=args.workload, stride=stride)
+                         bin_kmax=args.bin_kmax, workload=args.workload, stride=stride, max_cells=args.max_cells)
     n_sets = len(spec.rates)
     ctx = engine.Context(spec)
     hist = torch.zeros(n_sets * spec.hist_bins, dtype=torch.int64, device="cuda")

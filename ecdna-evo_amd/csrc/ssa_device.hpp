@@ -167,9 +167,9 @@ __device__ __forceinline__ void stage_logtab(double2* lds) {
     __syncthreads();
 }
 
-// Stream words of one event (draw mapping v3): [w2, w3, spare0 .. spare(nsp-1), blk1.x,
+// Stream words of one event (draw mapping v5): [w2, w3, spare0 .. spare(nsp-1), blk1.x,
 // blk1.y, blk1.z, blk1.w, blk2.x, ...], blk j = Philox(e, j, rid). The spares are words of earlier events'
-// blocks that no draw used (at most 2, oldest first). Only the rare paths (Lemire rejection, copy
+// blocks that no draw used, a two-slot stack (newest first). Only the rare paths (Lemire rejection, copy
 // numbers beyond what w3 and the spares cover, NoUneven redraws) reach the Philox blocks.
 // pos = words consumed so far; w2 counts as consumed by the cell pick (pos starts at 1).
 struct WordStream {
@@ -237,20 +237,19 @@ struct WordStream {
     }
 };
 
-// Spare words after an event that consumed `used` stream words (0 when no cell was picked): the
-// unconsumed spares (in order), then the event's unconsumed w2 / w3, keeping the first two.
+// The spare stack after an event that consumed `used` stream words (0 when no cell was picked), draw mapping
+// v5: the unused base words are pushed, newest on top (the oldest falls off the two slots): w2 then w3 when
+// used == 0, w3 when used == 1; used == 2 leaves the stack; used >= 3 consumed used - 2 words after w3, the
+// top spares first. Branch-free selects (v3 kept the oldest two in list order: ~15 more VALU per event; v4's
+// single spare sent 3.5x more events to a second Philox block, a net loss at C3).
 __device__ __forceinline__ void spares_update(uint32_t used, uint32_t w2, uint32_t w3, uint32_t& s0, uint32_t& s1,
                                               uint32_t& nsp) {
-    const uint32_t took = used > 2u ? min(used - 2u, nsp) : 0u;  // spares consumed
-    uint32_t a = took == 0u ? s0 : s1;                            // the list after dropping them
-    uint32_t n = nsp - took;
-    // append the unconsumed base words: w2 (used == 0), w3 (used <= 1)
-    const uint32_t x0 = used == 0u ? w2 : w3;
-    const uint32_t nx = used == 0u ? 2u : (used == 1u ? 1u : 0u);
-    const uint32_t b = n == 0u ? (nx >= 2u ? w3 : 0u) : x0;  // second slot
-    s0 = n == 0u ? x0 : a;
-    s1 = n >= 2u ? s1 : b;
-    nsp = min(n + nx, 2u);
+    const bool u0 = used == 0u, u1 = used == 1u, pop = used >= 3u;
+    const uint32_t c = used - 2u;  // words consumed past w3 (when pop)
+    const uint32_t n1 = s1, n0 = s0;
+    s1 = u0 ? w2 : (u1 ? n0 : n1);
+    s0 = (u0 || u1) ? w3 : (pop ? n1 : n0);
+    nsp = u0 ? 2u : (u1 ? min(nsp + 1u, 2u) : (pop ? (nsp > c ? nsp - c : 0u) : nsp));
 }
 
 }  // namespace ecdna

@@ -104,11 +104,11 @@ double oracle_softlog_neg(uint32_t w) {
 
 /* ------------------------------------------------------------ word stream */
 
-/* Per-event stream words (draw mapping v3): [w2, w3, spare[0], .., spare[nsp-1], blk1.x, blk1.y, blk1.z,
+/* Per-event stream words (draw mapping v5): [w2, w3, spare[0], .., spare[nsp-1], blk1.x, blk1.y, blk1.z,
  * blk1.w, blk2.x, ...] where blk j = Philox(ctr = (e, j, rid lo, rid hi)) and the spares are words of
- * earlier events' blocks that no draw consumed (at most 2, oldest first; spares_update()). Each word
- * is used at most once and whether it is used depends only on draws already made, so every draw
- * stays an independent uniform. pos = words consumed. */
+ * earlier events' blocks that no draw consumed, kept as a two-slot stack (newest first; spares_update()).
+ * Each word is used at most once and whether it is used depends only on draws already made, so every
+ * draw stays an independent uniform. pos = words consumed. */
 typedef struct {
     uint32_t key[2];
     uint32_t e, rid_lo, rid_hi;
@@ -200,18 +200,29 @@ static int segregate(wstream* s, int seg, uint32_t n, uint32_t* k1, int* uneven)
     return -1;
 }
 
-/* After an event that consumed `used` stream words: spares = (the unconsumed spares, in order) followed by
- * the event's unconsumed base words (w2 if used == 0, then w3 if used <= 1), truncated to the first two. */
+/* After an event that consumed `used` stream words (mapping v5): the unused base words are pushed on a
+ * two-slot stack (newest on top, the oldest falls off): w2 then w3 when used == 0, w3 when used == 1;
+ * used == 2 leaves it; used >= 3 consumed used - 2 words after w3, the top spares first. (v3 kept the
+ * oldest two in a list, v4 a single spare: the list cost ~15 VALU per event on the GPU, the single spare
+ * sent 3.5x more events to a second Philox block.) */
 static void spares_update(uint32_t sp[2], uint32_t* nsp, uint32_t used, uint32_t w2, uint32_t w3) {
-    uint32_t took = used > 2 ? used - 2 : 0;
-    if (took > *nsp) took = *nsp;
-    uint32_t list[4], n = 0;
-    for (uint32_t i = took; i < *nsp; ++i) list[n++] = sp[i];
-    if (used == 0) list[n++] = w2;
-    if (used <= 1) list[n++] = w3;
-    if (n > 2) n = 2;
-    for (uint32_t i = 0; i < n; ++i) sp[i] = list[i];
-    *nsp = n;
+    if (used == 0) {
+        sp[1] = w2;
+        sp[0] = w3;
+        *nsp = 2;
+    } else if (used == 1) {
+        sp[1] = sp[0];
+        sp[0] = w3;
+        *nsp = *nsp + 1 > 2 ? 2 : *nsp + 1;
+    } else if (used >= 3) {
+        const uint32_t c = used - 2;
+        if (*nsp > c) {
+            sp[0] = sp[1];
+            *nsp -= c;
+        } else {
+            *nsp = 0;
+        }
+    }
 }
 
 static void ws_init(wstream* s, uint64_t seed, uint64_t rid, uint32_t e, uint32_t w2, uint32_t w3) {
@@ -463,7 +474,7 @@ static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16
                                ecdna_rep_summary_t* out, ecdna_snapshot_t* snap_meta, uint16_t* snap_rows,
                                uint64_t snap_stride) {
     uint32_t sj = 0;
-    uint32_t spare[2] = {0, 0}, nspare = 0; /* spare stream words (draw mapping v3) */
+    uint32_t spare[2] = {0, 0}, nspare = 0; /* spare stream words (draw mapping v5) */
     const uint64_t set = rid / p->reps_per_set;
     const ecdna_rates_t rt = p->rates[set];
     const int bd = p->process == ECDNA_BIRTH_DEATH;

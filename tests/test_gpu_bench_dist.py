@@ -30,13 +30,13 @@ def _free_port():
     return p
 
 
-def _torchrun(nproc, reps_per_gpu, dump, extra_env):
+def _torchrun(nproc, reps_per_gpu, dump, extra_env, extra_args=()):
     env = dict(os.environ)
     env.update(extra_env)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
            "--gpus", str(nproc), "--steps", "2", "--warmup", "1", "--reps-per-gpu", str(reps_per_gpu),
-           "--no-cpu-baseline", "--dump-hist", str(dump)]
+           "--no-cpu-baseline", "--dump-hist", str(dump), *extra_args]
     out = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
@@ -77,3 +77,40 @@ def test_bench_distributed_paths_match_one_process(tmp_path):
         np.testing.assert_array_equal(d["hist"], ref_hist)
         np.testing.assert_array_equal(d["totals"].astype(np.int64), ref_tot)
     assert one["config"]["events_per_step"] == two["config"]["events_per_step"] == int(ref_tot[1])
+
+
+# the strong-scaling lines BASELINE.json places on 8 GPUs (C4: the ABC sweep's interleaved shards with the cost
+# hint's start order; C5: the turnover run), scaled down: (total replicates, cell cap)
+STRONG = {"c4": (1024 * 16, None), "c5": (512, 20_000), "c2": (4096, 2_000)}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workload", sorted(STRONG))
+def test_bench_strong_scaling_paths_match_one_process(tmp_path, workload):
+    """bench.py --workload c2/c4/c5 under torchrun: one rank over RCCL, and two ranks sharing cuda:0 over gloo
+    (interleaved global-id shards g, g + 2, ...; C4 with its per-set cost hint). The reduced histogram and
+    totals equal one engine run of every id bit for bit, and the line reports strong scaling."""
+    total, cells = STRONG[workload]
+    extra = ["--workload", workload, "--total", str(total)] + (["--max-cells", str(cells)] if cells else [])
+    one = _torchrun(1, 0, tmp_path / "one.npz", {}, extra)
+    two = _torchrun(2, 0, tmp_path / "two.npz", {"ECDNA_BENCH_BACKEND": "gloo", "ECDNA_BENCH_ONE_DEVICE": "1"}, extra)
+    for line, n in ((one, 1), (two, 2)):
+        assert line["n_gpus"] == n and line["scaling"] == "strong" and line["config"]["replicates_total"] == total
+        assert line["config"]["replicate_errors"] == 0
+
+    sys.path.insert(0, REPO)
+    import bench
+    from ecdna_evo_amd import engine
+
+    ctx = engine.Context(bench.workload_spec(0, total, total, workload=workload, max_cells=cells))
+    ctx.launch()
+    ctx.sync()
+    res = ctx.download()
+    ctx.close()
+    ref_hist = res.hist.astype(np.int64).reshape(-1)
+    ref_tot = res.totals.view(np.uint64).astype(np.int64).reshape(-1)
+    for f in ("one.npz", "two.npz"):
+        d = np.load(tmp_path / f)
+        np.testing.assert_array_equal(d["hist"], ref_hist, err_msg=f)
+        np.testing.assert_array_equal(d["totals"].astype(np.int64), ref_tot, err_msg=f)
+    assert one["config"]["events_per_step"] == two["config"]["events_per_step"] == int(ref_tot.reshape(-1, 16)[:, 1].sum())

@@ -11,7 +11,7 @@ trap 'rm -rf "$TMP"' EXIT
 if [ "$REF" = WORKTREE ]; then mkdir -p "$TMP/ecdna-evo_amd"; cp -r "$ROOT/ecdna-evo_amd/csrc" "$TMP/ecdna-evo_amd/"; cp -r "$ROOT/include" "$TMP/"; else git -C "$ROOT" archive "$REF" ecdna-evo_amd/csrc include | tar -x -C "$TMP"; fi
 mkdir -p "$OUT"
 cd "$TMP/ecdna-evo_amd"
-for f in csrc/ssa_kernels.hip csrc/ssa_api.cpp; do
+for f in csrc/*.hip csrc/*.cpp; do
   x=""; [ "${f##*.}" = cpp ] && x="-x hip"
   /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -ffp-contract=off ${EXTRA:-} $x -c "$f" -o "$TMP/$(basename "$f").o"
 done
@@ -19,5 +19,5 @@ if grep -q ECDNA_ILP_BUILD csrc/ssa_kernels.hip; then  # (refs since the two-sch
   /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -ffp-contract=off ${EXTRA:-} -DECDNA_ILP_BUILD \
     -mllvm -amdgpu-sched-strategy=max-ilp -c csrc/ssa_kernels.hip -o "$TMP/ssa_kernels_ilp.o"
 fi
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libecdna_ssa.so" "$TMP"/*.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libecdna_ssa.so" "$TMP"/*.o -ldl
 echo "$OUT/libecdna_ssa.so"
