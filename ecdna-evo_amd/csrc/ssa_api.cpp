@@ -176,7 +176,7 @@ struct ecdna_ssa_ctx {
     // per-replicate final counters [chunk_reps][bin_k]
     uint32_t bin_k = 0;
     int bin_c32 = 0;
-    int bin_ilp = 0;  // the bin stepper's schedule: 0 default, 1 max-ILP (lone waves), 2 128-VGPR K = 64 (ssa_launch.h)
+    int bin_ilp = 0;  // the bin stepper's schedule: 0 default, 1 max-ILP (lone waves), 2 128-VGPR K = 64, 3 max-ILP paired lanes (ssa_launch.h)
     void* d_bags = nullptr;
     uint32_t stepper_block = ecdna::kStepperBlock;
     // reference draws (ECDNA_FLAG_REFERENCE_DRAWS): the ChaCha8 key and the BTPE constants per copy number
@@ -533,7 +533,17 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
         CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &occ_ilp, ecdna::bin_stepper_kernel(p->process, p->segregation, c->bin_k, c->bin_c32, p->flags, 1),
             (int)c->stepper_block, 0));
-        if (sched == 1 || (sched == 2 && max_chunk <= (uint64_t)c->cus * 256u))
+        // Paired lanes: with at most half a wave of replicates per SIMD (the C5 8-GPU shard) the
+        // idle half of each wave computes the next event's Philox block and soft log in the N- fast-forward.
+        // Birth-death without snapshots (the fast-forward's domain). ECDNA_SSA_PAIR = 0 off, 1 whenever
+        // possible, 2 auto.
+        const uint64_t pair_mode = env_u64("ECDNA_SSA_PAIR", 2);
+        const bool pair_ok = p->process == ECDNA_BIRTH_DEATH && p->n_snapshots == 0 &&
+                             ecdna::bin_stepper_kernel_pair(p->segregation, c->bin_k, c->bin_c32, p->flags) != nullptr;
+        if (pair_ok && (pair_mode == 1 ||
+                        (pair_mode == 2 && sched == 2 && max_chunk <= (uint64_t)c->cus * (ecdna::kStepperBlock / 2))))
+            c->bin_ilp = 3;
+        else if (sched == 1 || (sched == 2 && max_chunk <= (uint64_t)c->cus * 256u))
             c->bin_ilp = 1;
         else if (k64u16 && (sched == 3 || (sched == 2 && tf0 && max_chunk >= 4ull * c->cus * 4u * ecdna::kStepperBlock)))
             c->bin_ilp = 2;
@@ -671,7 +681,8 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
         a.snap_stride = c->out_stride;
         a.big_cap = c->big_cap;
         a.bags = c->d_bags;
-        const uint32_t need = (ch.n + c->stepper_block - 1) / c->stepper_block;
+        const uint32_t per_block = c->bin_ilp == 3 ? c->stepper_block / 2 : c->stepper_block;  // (paired: owners)
+        const uint32_t need = (ch.n + per_block - 1) / per_block;
         const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(need, c->stepper_blocks_cap));
         // Drain control (bin store, 256-lane blocks, one wave per SIMD per block): when lanes run more than
         // two replicates each, the youngest wave slot of every SIMD stops taking fresh replicates once

@@ -562,7 +562,10 @@ __device__ __forceinline__ uint32_t vec_get(const uint4& v, int j) {
 
 // SCH: the build's schedule (no code): 0 occupancy-first, 1 max-ILP (ECDNA_ILP_BUILD), 2 occupancy-first
 // capped at 128 VGPRs so that four 256-lane workgroups fit a CU (K = 64 / u16 only, many replicates per lane)
-template <bool BD, int SEG, int NG, bool C32, int BLK, int TF, int SCH>
+// PAIR (lone waves, DESIGN.md §5 "Paired lanes"): lane l < 32 of every wave owns a replicate, lane l + 32 is
+// its helper: in the N- fast-forward both compute a Philox block and soft log with the same instructions, the
+// owner's for event e and the helper's for e + 1, and the owner runs both events' state-dependent steps.
+template <bool BD, int SEG, int NG, bool C32, int BLK, int TF, int SCH, bool PAIR = false>
 __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const StepperArgs a) {
     using L = BinLayout<NG, C32>;
     constexpr uint32_t K = L::kK;
@@ -576,6 +579,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
     PhiloxEventPre pre{0u, 0u, 0u};  // the replicate-only part of round 0
     PATH_STATS_DECL;
     const uint32_t stop32 = a.stop_cells < 0xffffffffull ? (uint32_t)a.stop_cells : 0xffffffffu;
+    const bool helper = PAIR && (threadIdx.x & 63u) >= 32u;  // PAIR: serves lane - 32, never owns a replicate
 
     // packed counter add: bin b (0-based, copy number b + 1) / group g, by +d (d = +1, -1 or 0, as a
     // two's complement 32-bit word: a 16-bit field never borrows from its neighbour because it is >= 1
@@ -740,6 +744,14 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
 #endif
     for (;;) {
         ++ff_tick;
+        // PAIR: a helper leaves with the last owner of its wave (EXEC at the reconverged loop top holds the lanes
+        // still looping; owners are its low 32 bits). Read before the helper-only branch, whose EXEC would hide
+        // the owners (volatile: it is not sunk into the branch).
+        if (PAIR) {
+            uint64_t live;
+            asm volatile("s_mov_b64 %0, exec" : "=s"(live));
+            if (helper && (uint32_t)live == 0u) break;
+        }
         if (rot && ((++it & tick_mask) == 0u)) {  // ---- rotation tick (wave-uniform)
 #ifdef ECDNA_ROT_STATS
             const unsigned long long c0 = clock64();
@@ -780,7 +792,8 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
         const unsigned long long cb0 = clock64();
         const bool any_bound = __builtin_amdgcn_read_exec() & __ballot(!active);
 #endif
-        if (!active) {  // ---- replicate boundary (rare): write the finished one, pull the next
+        // (a PAIR helper claims nothing: it skips the boundary and takes part in the fast-forward steps below)
+        if (!active && !(PAIR && helper)) {  // ---- replicate boundary (rare): write the finished one, pull the next
             KArgs* const ra = rare_args();
             if (have) {
                 store_bag();
@@ -947,7 +960,67 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
             const bool heavy = active && pm * 8.0 >= (pm + pbf + pdf) * (double)ECDNA_FF_ENTER8;
             const uint32_t n_in = (uint32_t)__builtin_popcountll(__ballot(active));
             ff_mode = n_in != 0u && (uint32_t)__builtin_popcountll(__ballot(heavy)) * 8u >= n_in * ECDNA_FF_ENTER8;
-            if (ff_mode) {
+            if (PAIR && ff_mode) {
+                // Paired steps (DESIGN.md §5 "Paired lanes"): every lane forms one Philox block and soft log with
+                // the same instructions, the owner (lane l) for its event e, the helper (lane l + 32) for the
+                // owner's e + 1 from the owner's replicate-only round-0 words; the owner pulls the helper's words
+                // (v_permlane32_swap) and runs the state-dependent part of e, then of e + 1. Same draws, same
+                // arithmetic, same order as the unpaired loop below: results are identical.
+                bool go = active;
+                PhiloxEventPre hp = pre;
+                {
+                    const auto x0 = __builtin_amdgcn_permlane32_swap(pre.x0, pre.x0, false, false);
+                    const auto x1 = __builtin_amdgcn_permlane32_swap(pre.x1, pre.x1, false, false);
+                    const auto x2 = __builtin_amdgcn_permlane32_swap(pre.x2, pre.x2, false, false);
+                    if (helper) hp = PhiloxEventPre{x0[0], x1[0], x2[0]};  // (lanes >= 32 receive lanes < 32)
+                }
+                // one event of the fast-forward: the unpaired loop's body with the block words and soft log given
+                auto ff_event = [&](uint32_t wy, uint32_t wz, uint32_t ww, double softlog) {
+                    const double fm2 = (double)nm;
+                    const double cA2 = rb0 * fm2;
+                    const double cB2 = cA2 + pbf;
+                    const double cC2 = cB2 + rd0 * fm2;
+                    const double a02 = cC2 + pdf;
+                    const bool t_over2 = f32t ? (t32 >= a.max_time32) : (t >= a.max_time);
+                    if ((e >= a.max_iter) || nm + npf >= stop32 || t_over2 || !(a02 > 0.0)) {
+                        go = false;
+                        return;
+                    }
+                    const double target2 = fma3((double)wy, 0x1p-32, 0x1p-33) * a02;
+                    const uint32_t ch2 = (target2 >= cA2 ? 1u : 0u) + (target2 >= cB2 ? 1u : 0u) +
+                                         (target2 >= cC2 ? 1u : 0u);
+                    if (ch2 & 1u) {
+                        go = false;
+                        return;
+                    }
+                    const double tau2 = div_in_range(softlog, a02);
+                    spares_update(0u, wz, ww, sp0, sp1, nsp);
+                    nm = nm + (ch2 == 0u ? 1u : 0u) - (ch2 == 2u ? 1u : 0u);
+                    n_dm += ch2 == 2u ? 1u : 0u;
+                    e += 1;
+                    if (f32t)
+                        t32 = t32 + (float)tau2;
+                    else
+                        t = t + tau2;
+                    if (hash_on) h = (h ^ (uint64_t)ch2) * kFnvPrime;
+                };
+#pragma unroll 1
+                for (uint32_t q = 0; q < kFfMax; q += 2) {
+                    if ((uint32_t)__builtin_popcountll(__ballot(go)) * 8u < n_in * ECDNA_FF_STAY8) break;  // (uniform)
+                    const uint32_t eo = __builtin_amdgcn_permlane32_swap(e, e, false, false)[0];
+                    const uint4 wb = helper ? philox_event(eo + 1u, hp, rk) : philox_event(e, pre, rk);
+                    const double lg = softlog_neg(wb.x, logtab);
+                    const uint64_t lgb = (uint64_t)__double_as_longlong(lg);
+                    const uint32_t lo2 = __builtin_amdgcn_permlane32_swap((uint32_t)lgb, (uint32_t)lgb, false, false)[1];
+                    const uint32_t hi2 =
+                        __builtin_amdgcn_permlane32_swap((uint32_t)(lgb >> 32), (uint32_t)(lgb >> 32), false, false)[1];
+                    const uint32_t y2 = __builtin_amdgcn_permlane32_swap(wb.y, wb.y, false, false)[1];
+                    const uint32_t z2 = __builtin_amdgcn_permlane32_swap(wb.z, wb.z, false, false)[1];
+                    const uint32_t w2 = __builtin_amdgcn_permlane32_swap(wb.w, wb.w, false, false)[1];
+                    if (go) ff_event(wb.y, wb.z, wb.w, lg);
+                    if (go) ff_event(y2, z2, w2, __longlong_as_double((long long)(((uint64_t)hi2 << 32) | lo2)));
+                }
+            } else if (ff_mode) {
                 bool go = active;
 #pragma unroll 1
                 for (uint32_t q = 0; q < kFfMax; ++q) {
@@ -1402,12 +1475,30 @@ static const void* const kBinOcc4Table[2][2][4] = {{ECDNA_BIN_OCC4(false, 0), EC
 const void* bin_stepper_kernel_ilp(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags) {
     return bin_table_entry(birth_death, segregation, bin_k, c32, flags);
 }
+
+// paired lanes (PAIR = true; birth-death only, its N- fast-forward is what pairs): [TF][segregation][K = 32 / u32,
+// K = 64 / u16, K = 64 / u32]
+#define ECDNA_BIN_PAIR_SEG(SEG, TF)                                                                          \
+    {(const void*)ssa_stepper_bins<true, SEG, 4, true, kStepperBlock, TF, ECDNA_SCH, true>,                 \
+     (const void*)ssa_stepper_bins<true, SEG, 8, false, kStepperBlock, TF, ECDNA_SCH, true>,                \
+     (const void*)ssa_stepper_bins<true, SEG, 8, true, kStepperBlock, TF, ECDNA_SCH, true>}
+#define ECDNA_BIN_PAIR_TF(TF) \
+    {ECDNA_BIN_PAIR_SEG(0, TF), ECDNA_BIN_PAIR_SEG(1, TF), ECDNA_BIN_PAIR_SEG(2, TF), ECDNA_BIN_PAIR_SEG(3, TF)}
+static const void* const kBinPairTable[2][4][3] = {ECDNA_BIN_PAIR_TF(0), ECDNA_BIN_PAIR_TF(1)};
+
+const void* bin_stepper_kernel_pair(int segregation, uint32_t bin_k, int c32, uint32_t flags) {
+    const int tf = (flags & (ECDNA_FLAG_TIME_F32 | ECDNA_FLAG_EVENT_HASH)) ? 1 : 0;
+    if (bin_k == 32 && c32) return kBinPairTable[tf][segregation & 3][0];
+    if (bin_k == 64) return kBinPairTable[tf][segregation & 3][c32 ? 2 : 1];
+    return nullptr;
+}
 #else
 const void* stepper_kernel(int birth_death, int segregation, int window) {
     return kStepperTable[window ? 1 : 0][birth_death ? 1 : 0][segregation & 3];
 }
 
 const void* bin_stepper_kernel(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags, int ilp) {
+    if (ilp == 3) return birth_death ? bin_stepper_kernel_pair(segregation, bin_k, c32, flags) : nullptr;
     if (ilp == 2 && bin_k == 64 && !c32) {
         const int tf = (flags & (ECDNA_FLAG_TIME_F32 | ECDNA_FLAG_EVENT_HASH)) ? 1 : 0;
         return kBinOcc4Table[tf][birth_death ? 1 : 0][segregation & 3];

@@ -123,6 +123,10 @@ hipError_t launch_stepper(const StepperArgs& a, int birth_death, int segregation
 // replicates each; other K / counter widths fall back to the default schedule.
 const void* bin_stepper_kernel(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags, int ilp);
 const void* bin_stepper_kernel_ilp(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags);
+// ilp = 3: the max-ILP schedule with paired lanes (lane l < 32 owns a replicate, lane l + 32 helps its N-
+// fast-forward; birth-death, K = 32 / u32 or K = 64): nullptr where no such instance exists. A paired
+// workgroup of kStepperBlock lanes runs kStepperBlock / 2 replicates at a time.
+const void* bin_stepper_kernel_pair(int segregation, uint32_t bin_k, int c32, uint32_t flags);
 int bin_stepper_block(uint32_t bin_k);
 hipError_t launch_bin_stepper(const StepperArgs& a, int birth_death, int segregation, uint32_t bin_k, int c32, int ilp,
                               uint32_t blocks, hipStream_t stream);

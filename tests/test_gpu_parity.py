@@ -223,6 +223,13 @@ def test_gpu_nminus_fast_forward_matches_oracle(name, engine_mod, oracle_mod, mo
     for sched in ("1", "0", "3"):
         monkeypatch.setenv("ECDNA_SSA_SCHED", sched)
         _compare(engine_mod.run(spec, want_rows=True), cpu, f"{name}/sched{sched}")
+    # paired lanes: the default here (auto: at most half a wave of replicates per SIMD), and forced
+    # onto two workgroups so that every owner lane runs several replicates one after another
+    monkeypatch.setenv("ECDNA_SSA_SCHED", "2")
+    _compare(engine_mod.run(spec, want_rows=True), cpu, f"{name}/auto")
+    monkeypatch.setenv("ECDNA_SSA_PAIR", "1")
+    monkeypatch.setenv("ECDNA_SSA_MAX_BLOCKS", "2")
+    _compare(engine_mod.run(spec, want_rows=True), cpu, f"{name}/pair-refill")
     s = cpu.summaries
     ev = s["events_by_type"].astype(np.int64)
     nminus_share = (ev[:, 0] + ev[:, 2]).sum() / ev.sum()
