@@ -245,11 +245,12 @@ struct WordStream {
 __device__ __forceinline__ void spares_update(uint32_t used, uint32_t w2, uint32_t w3, uint32_t& s0, uint32_t& s1,
                                               uint32_t& nsp) {
     const bool u0 = used == 0u, u1 = used == 1u, pop = used >= 3u;
-    const uint32_t c = used - 2u;  // words consumed past w3 (when pop)
     const uint32_t n1 = s1, n0 = s0;
     s1 = u0 ? w2 : (u1 ? n0 : n1);
-    s0 = (u0 || u1) ? w3 : (pop ? n1 : n0);
-    nsp = u0 ? 2u : (u1 ? min(nsp + 1u, 2u) : (pop ? (nsp > c ? nsp - c : 0u) : nsp));
+    s0 = (used <= 1u) ? w3 : (pop ? n1 : n0);
+    // 2 pushes (used 0), 1 push (used 1), none (used 2), used - 2 pops: min(max(nsp + 2 - used, 0), 2)
+    const uint32_t grown = nsp + 2u;
+    nsp = min(grown > used ? grown - used : 0u, 2u);
 }
 
 }  // namespace ecdna
