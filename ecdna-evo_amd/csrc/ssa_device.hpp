@@ -207,8 +207,9 @@ struct WordStream {
     // and spares the Philox blocks come from a lane-uniform loop, one block per iteration with its four
     // words popcounted branch-free. (Word by word, next() generates a block whenever ANY lane of the
     // wave crosses a block boundary, and lanes sit at different stream offsets: large copy numbers then
-    // ran a Philox block for almost every word. rk: the kernel's VGPR round keys, or nullptr.)
-    __device__ __forceinline__ uint32_t binomial_half(uint32_t n, const PhiloxKeys* rk = nullptr) {
+    // ran a Philox block for almost every word.) block(c): Philox4x32-10 of counter c under the run's key.
+    template <class Block>
+    __device__ __forceinline__ uint32_t binomial_half_with(uint32_t n, const Block& block) {
         uint32_t c = 0;
         while (n && pos < 2u + nsp) {  // w3 and the spares (at most three words; no Philox block here)
             const uint32_t p = pos++;
@@ -220,8 +221,7 @@ struct WordStream {
         while (n) {
             const uint32_t q = pos - 2u - nsp;  // stream offset inside the block region
             const uint32_t j = (q >> 2) + 1u;
-            const uint4 c4 = make_uint4(e, j, rid_lo, rid_hi);
-            blk = rk ? philox4x32_10(c4, *rk) : philox4x32_10(c4, k0, k1);
+            blk = block(make_uint4(e, j, rid_lo, rid_hi));
             blk_id = j;
             const uint32_t t0 = q & 3u;
             const uint32_t w[4] = {blk.x, blk.y, blk.z, blk.w};
@@ -234,6 +234,18 @@ struct WordStream {
             }
         }
         return c;
+    }
+
+    // with the key schedule formed per block (k0, k1)
+    __device__ __forceinline__ uint32_t binomial_half(uint32_t n) {
+        return binomial_half_with(n, [&](uint4 c4) { return philox4x32_10(c4, k0, k1); });
+    }
+
+    // with the kernel's VGPR round keys. (A reference, never a nullable pointer: a null test of the keys'
+    // private-memory address does not fold on AMDGPU, where private null is not address 0, and the test alone
+    // kept the 20 keys in scratch, reloaded at every Philox round of every kernel that had it.)
+    __device__ __forceinline__ uint32_t binomial_half(uint32_t n, const PhiloxKeys& rk) {
+        return binomial_half_with(n, [&](uint4 c4) { return philox4x32_10(c4, rk); });
     }
 };
 

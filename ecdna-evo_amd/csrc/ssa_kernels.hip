@@ -1155,7 +1155,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                 if (prolif && fast) ws.pos = fast1 ? 2u : 3u;
                 if (prolif && !fast && k <= 32767u) {  // larger copy numbers or a rejected pick: more words
                     PATH_STAT(5);
-                    k1v = ws.binomial_half(n, &rk);
+                    k1v = ws.binomial_half(n, rk);
                     if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN) {
                         uint32_t tries = 1;
                         while (k1v == 0u || k1v == n) {
@@ -1163,7 +1163,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                                 ev_err = ECDNA_REP_ERR_REJECTION;
                                 break;
                             }
-                            k1v = ws.binomial_half(n, &rk);
+                            k1v = ws.binomial_half(n, rk);
                             ++tries;
                         }
                     }
@@ -1174,7 +1174,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                             ev_err = ECDNA_REP_ERR_REJECTION;
                             break;
                         }
-                        k1v = ws.binomial_half(n, &rk);
+                        k1v = ws.binomial_half(n, rk);
                         ++tries;
                     }
                 }

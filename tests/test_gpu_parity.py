@@ -186,6 +186,21 @@ def test_gpu_bin_store_both_schedules_match_oracle(name, sched, engine_mod, orac
     _compare(engine_mod.run(spec, want_rows=True), oracle_mod.run(spec, mode="philox", want_rows=True), name)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("blocks", ["0", "2"])
+@pytest.mark.parametrize("name", sorted(BIN_CASES))
+def test_gpu_bin_store_paired_lanes_match_oracle(name, blocks, engine_mod, oracle_mod, monkeypatch):
+    """Paired lanes forced (ECDNA_SSA_PAIR = 1; DESIGN.md §5: in the N- fast-forward lane l < 32 runs events
+    e and e + 1, lane l + 32 forms the Philox block and soft log of e + 1) on every bin-store case, bit for bit
+    against the oracle; on the default grid and squeezed onto two workgroups (owners refill many times). The
+    kernels without a paired instance (pure birth, K = 256, snapshots) run unpaired and must match all the same."""
+    monkeypatch.setenv("ECDNA_SSA_PAIR", "1")
+    if blocks != "0":
+        monkeypatch.setenv("ECDNA_SSA_MAX_BLOCKS", blocks)
+    spec = BIN_CASES[name]
+    _compare(engine_mod.run(spec, want_rows=True), oracle_mod.run(spec, mode="philox", want_rows=True), name)
+
+
 def _nminus_heavy_specs():
     """Populations that become mostly N- (N- fitter than N+; uneven splits of k = 1 cells feed it), so the
     N- fast-forward runs most events; stops that land inside it (max_iter, max_time,

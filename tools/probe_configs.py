@@ -1,6 +1,6 @@
 """Throughput of the engine on every BASELINE.json config shape that runs on one GPU
 (configs[1..4]; C4 and C5 as the per-GPU shard of their 8-GPU runs). Development/measurement tool.
-Usage: [PROBE_FLAGS=0x20] [PROBE_KMAX=256] [PROBE_RANK=r] [PROBE_GPUS=8] python tools/probe_configs.py [c2 c3 c4 c5]"""
+Usage: [PROBE_FLAGS=0x20] [PROBE_KMAX=256] [PROBE_SEG=s] [PROBE_RANK=r] [PROBE_GPUS=8] python tools/probe_configs.py [c2 c3 c4 c5]"""
 import dataclasses
 import json
 import os
@@ -55,6 +55,8 @@ def main():
         spec = CONFIGS[name](int(os.environ.get("PROBE_RANK", "0")), gpus) if name in ("c4", "c5") else CONFIGS[name]()
         spec = dataclasses.replace(spec, flags=spec.flags | int(os.environ.get("PROBE_FLAGS", "0"), 0),
                                    bin_kmax=int(os.environ.get("PROBE_KMAX", "0")), _keep=[])
+        if "PROBE_SEG" in os.environ:  # another segregation rule (abi.SEG_*) on the same shape
+            spec = dataclasses.replace(spec, segregation=int(os.environ["PROBE_SEG"]), _keep=[])
         t0 = time.time()
         ctx = engine.Context(spec)
         reps = 1 if name == "c5" else 2
