@@ -236,6 +236,58 @@ struct WordStream {
         return c;
     }
 
+    // The no-uneven rule's redraws for 2 <= n <= 32 (SEG_BINOMIAL_NO_UNEVEN: resample k1 while it is 0 or n,
+    // src/segregation.rs:157-174), after `tries` rejected draws: the same words in the same order as repeated
+    // binomial_half(n) calls (one word per try), but the accepted word is found branch-free over the base
+    // words and then four words at a time over Philox blocks, one block per iteration of a lane loop (a word
+    // is rejected with probability 2^(1-n) <= 1/2: word by word the wave looped once per try of its unluckiest
+    // lane, each try a full binomial_half). `fail`: max_tries draws, all uneven (ECDNA_REP_ERR_REJECTION).
+    template <class Block>
+    __device__ __forceinline__ uint32_t redraw_even_small_with(uint32_t n, uint32_t tries, uint32_t max_tries,
+                                                               bool& fail, const Block& block) {
+        const uint32_t m = low_bits(n);
+        uint32_t res = 0;
+        bool found = false;
+        const auto try_word = [&](uint32_t w, bool take) {
+            const uint32_t c = __popc(w & m);
+            const bool acc = take && c != 0u && c != n;
+            res = acc ? c : res;
+            found = found || acc;
+            tries += take ? 1u : 0u;
+        };
+#pragma unroll
+        for (uint32_t p = 1; p < 4u; ++p) {  // w3 (position 1) and the spares (2, 3)
+            const bool take = !found && p >= pos && p < 2u + nsp && tries < max_tries;
+            try_word(p == 1u ? w3 : sel(p == 2u, s0, s1), take);
+            pos = take ? p + 1u : pos;
+        }
+        while (!found && tries < max_tries) {
+            const uint32_t q = pos - 2u - nsp;
+            const uint32_t j = (q >> 2) + 1u;
+            blk = block(make_uint4(e, j, rid_lo, rid_hi));
+            blk_id = j;
+            const uint32_t t0 = q & 3u;
+            const uint32_t w[4] = {blk.x, blk.y, blk.z, blk.w};
+#pragma unroll
+            for (uint32_t t = 0; t < 4u; ++t) {
+                const bool take = !found && t >= t0 && tries < max_tries;
+                try_word(w[t], take);
+                pos += take ? 1u : 0u;
+            }
+        }
+        fail = !found;
+        return res;
+    }
+
+    __device__ __forceinline__ uint32_t redraw_even_small(uint32_t n, uint32_t tries, uint32_t max_tries, bool& fail) {
+        return redraw_even_small_with(n, tries, max_tries, fail, [&](uint4 c4) { return philox4x32_10(c4, k0, k1); });
+    }
+
+    __device__ __forceinline__ uint32_t redraw_even_small(uint32_t n, uint32_t tries, uint32_t max_tries, bool& fail,
+                                                          const PhiloxKeys& rk) {
+        return redraw_even_small_with(n, tries, max_tries, fail, [&](uint4 c4) { return philox4x32_10(c4, rk); });
+    }
+
     // with the key schedule formed per block (k0, k1)
     __device__ __forceinline__ uint32_t binomial_half(uint32_t n) {
         return binomial_half_with(n, [&](uint4 c4) { return philox4x32_10(c4, k0, k1); });

@@ -319,13 +319,17 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
                 if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN) {
                     uint32_t tries = 1;
                     bool rej = false;
-                    while (k1v == 0u || k1v == n) {
-                        if (tries == kNoUnevenMaxTries) {
-                            rej = true;
-                            break;
+                    if (n <= 32u && (k1v == 0u || k1v == n)) {
+                        k1v = ws.redraw_even_small(n, tries, kNoUnevenMaxTries, rej);
+                    } else {
+                        while (k1v == 0u || k1v == n) {
+                            if (tries == kNoUnevenMaxTries) {
+                                rej = true;
+                                break;
+                            }
+                            k1v = ws.binomial_half(n);
+                            ++tries;
                         }
-                        k1v = ws.binomial_half(n);
-                        ++tries;
                     }
                     if (rej) {
                         err = ECDNA_REP_ERR_REJECTION;
@@ -1156,7 +1160,14 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                 if (prolif && !fast && k <= 32767u) {  // larger copy numbers or a rejected pick: more words
                     PATH_STAT(5);
                     k1v = ws.binomial_half(n, rk);
-                    if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN) {
+                }
+                if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN && prolif && (k1v == 0u || k1v == n)) {
+                    // src/segregation.rs:157-174: redraw while uneven (the first draw above was try 1)
+                    if (n <= 32u) {
+                        bool fail = false;
+                        k1v = ws.redraw_even_small(n, 1u, kNoUnevenMaxTries, fail, rk);
+                        if (fail) ev_err = ECDNA_REP_ERR_REJECTION;
+                    } else {
                         uint32_t tries = 1;
                         while (k1v == 0u || k1v == n) {
                             if (tries == kNoUnevenMaxTries) {
@@ -1166,16 +1177,6 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                             k1v = ws.binomial_half(n, rk);
                             ++tries;
                         }
-                    }
-                } else if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN && prolif) {
-                    uint32_t tries = 1;
-                    while (k1v == 0u || k1v == n) {
-                        if (tries == kNoUnevenMaxTries) {
-                            ev_err = ECDNA_REP_ERR_REJECTION;
-                            break;
-                        }
-                        k1v = ws.binomial_half(n, rk);
-                        ++tries;
                     }
                 }
                 if (SEG != ECDNA_SEG_BINOMIAL_NO_UNEVEN)

@@ -201,6 +201,36 @@ def test_gpu_bin_store_paired_lanes_match_oracle(name, blocks, engine_mod, oracl
     _compare(engine_mod.run(spec, want_rows=True), oracle_mod.run(spec, mode="philox", want_rows=True), name)
 
 
+def _no_uneven_small_specs():
+    """The no-uneven rule's redraws at small copy numbers (n = 2k <= 32: a draw is rejected with probability
+    2^(1-n), so k = 1 cells redraw about once per division and reach the spares and then Philox blocks):
+    both processes, both stores, K = 32 and 64, spares refilled by N- and death events."""
+    out = {}
+    for i, (proc, rates, init) in enumerate([
+            (abi.PURE_BIRTH, (1.0, 1.0, 0.0, 0.0), {1: 1}),
+            (abi.BIRTH_DEATH, (1.0, 1.5, 0.3, 0.3), {1: 3, 2: 2, 16: 1}),
+            (abi.BIRTH_DEATH, (1.4, 1.0, 0.6, 0.2), {1: 4, 0: 3}),
+    ]):
+        for store, kmax in (("rows", 0), ("bins", 32), ("bins", 64)):
+            flags = H | (abi.FLAG_BIN_STORE if store == "bins" else 0)
+            out[f"nu{i}_{store}{kmax or ''}"] = abi.RunSpec(
+                seed=110 + i, process=proc, segregation=abi.SEG_BINOMIAL_NO_UNEVEN, rates=(rates,), init=init,
+                n_replicates=300, max_cells=1200, bin_kmax=kmax, flags=flags)
+    return out
+
+
+NU_SPECS = _no_uneven_small_specs()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(NU_SPECS))
+def test_gpu_no_uneven_small_redraws_match_oracle(name, engine_mod, oracle_mod):
+    """ssa_device.hpp's redraw_even_small (the accepted word found branch-free over the base words, then four
+    at a time over Philox blocks) against the oracle's try-by-try loop, bit for bit."""
+    spec = NU_SPECS[name]
+    _compare(engine_mod.run(spec, want_rows=True), oracle_mod.run(spec, mode="philox", want_rows=True), name)
+
+
 def _nminus_heavy_specs():
     """Populations that become mostly N- (N- fitter than N+; uneven splits of k = 1 cells feed it), so the
     N- fast-forward runs most events; stops that land inside it (max_iter, max_time,
