@@ -478,6 +478,43 @@ ECDNA_DEV_STATIC __device__ unsigned long long g_path_stats[8];
 #define PATH_STATS_FLUSH() ((void)0)
 #endif
 
+// Development cycle counters of the bin stepper's loop sections (built with -DECDNA_CYCLE_STATS only;
+// tools/cycle_stats.py), per wave, summed over waves: [0] shader-clock cycles from the loop top through the
+// replicate boundary, [1] the fast-forward block (entry test included), [2] the full event and the loop
+// latch, [3] iterations, [4] fast-forward entries, [5] fast-forward steps, [6] lanes entering the full event,
+// [7] whole-kernel cycles. Marks sit at wave-uniform points; the wave's lane 0 flushes.
+#ifdef ECDNA_CYCLE_STATS
+#ifdef ECDNA_ILP_BUILD
+#define ECDNA_CYC_SYM g_cycle_stats_ilp
+#else
+#define ECDNA_CYC_SYM g_cycle_stats
+#endif
+ECDNA_DEV_STATIC __device__ unsigned long long ECDNA_CYC_SYM[8];
+#define CYC_DECL                                                                                               \
+    unsigned long long cy_[8] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull};                              \
+    const unsigned long long cy_start_ = clock64();                                                           \
+    unsigned long long cy_t_ = cy_start_
+#define CYC_MARK(i)                                                                                            \
+    do {                                                                                                       \
+        const unsigned long long n_ = clock64();                                                               \
+        cy_[i] += n_ - cy_t_;                                                                                  \
+        cy_t_ = n_;                                                                                            \
+    } while (0)
+#define CYC_ADD(i, v) (cy_[i] += (unsigned long long)(v))
+#define CYC_FLUSH()                                                                                            \
+    do {                                                                                                       \
+        cy_[7] = clock64() - cy_start_;                                                                        \
+        if ((threadIdx.x & 63u) == 0u)                                                                         \
+            for (int q = 0; q < 8; ++q)                                                                        \
+                __hip_atomic_fetch_add(&ECDNA_CYC_SYM[q], cy_[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   \
+    } while (0)
+#else
+#define CYC_DECL
+#define CYC_MARK(i) ((void)0)
+#define CYC_ADD(i, v) ((void)0)
+#define CYC_FLUSH() ((void)0)
+#endif
+
 // The kernel argument block as seen from a rare path: read through a pointer the compiler cannot prove
 // loop-invariant, so those loads stay inside the rare block instead of holding scalar registers across
 // the event loop (the bin stepper's event path already fills the SGPR file).
@@ -746,7 +783,10 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
 #ifdef ECDNA_ROT_STATS
     unsigned long long c_tick = 0, c_bound = 0, c_start = clock64();
 #endif
+    CYC_DECL;
     for (;;) {
+        CYC_MARK(2);
+        CYC_ADD(3, 1);
         ++ff_tick;
         // PAIR: a helper leaves with the last owner of its wave (EXEC at the reconverged loop top holds the lanes
         // still looping; owners are its low 32 bits). Read before the helper-only branch, whose EXEC would hide
@@ -948,6 +988,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
 #ifdef ECDNA_ROT_STATS
         if (any_bound) c_bound += clock64() - cb0;
 #endif
+        CYC_MARK(0);
         // ---- N- fast-forward (birth-death; DESIGN.md §5 "N- fast-forward"): an N- event
         // (ProliferateNMinus, DeathNMinus) picks no cell, so its exact work is the propensities, the stop
         // checks, the block, the channel, the time step and the n- / spare / count / hash updates. While
@@ -964,6 +1005,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
             const bool heavy = active && pm * 8.0 >= (pm + pbf + pdf) * (double)ECDNA_FF_ENTER8;
             const uint32_t n_in = (uint32_t)__builtin_popcountll(__ballot(active));
             ff_mode = n_in != 0u && (uint32_t)__builtin_popcountll(__ballot(heavy)) * 8u >= n_in * ECDNA_FF_ENTER8;
+            CYC_ADD(4, ff_mode ? 1u : 0u);
             if (PAIR && ff_mode) {
                 // Paired steps (DESIGN.md §5 "Paired lanes"): every lane forms one Philox block and soft log with
                 // the same instructions, the owner (lane l) for its event e, the helper (lane l + 32) for the
@@ -978,42 +1020,28 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     const auto x2 = __builtin_amdgcn_permlane32_swap(pre.x2, pre.x2, false, false);
                     if (helper) hp = PhiloxEventPre{x0[0], x1[0], x2[0]};  // (lanes >= 32 receive lanes < 32)
                 }
-                // one event of the fast-forward: the unpaired loop's body with the block words and soft log given
-                auto ff_event = [&](uint32_t wy, uint32_t wz, uint32_t ww, double softlog) {
-                    const double fm2 = (double)nm;
-                    const double cA2 = rb0 * fm2;
-                    const double cB2 = cA2 + pbf;
-                    const double cC2 = cB2 + rd0 * fm2;
-                    const double a02 = cC2 + pdf;
-                    const bool t_over2 = f32t ? (t32 >= a.max_time32) : (t >= a.max_time);
-                    if ((e >= a.max_iter) || nm + npf >= stop32 || t_over2 || !(a02 > 0.0)) {
-                        go = false;
-                        return;
-                    }
-                    const double target2 = fma3((double)wy, 0x1p-32, 0x1p-33) * a02;
-                    const uint32_t ch2 = (target2 >= cA2 ? 1u : 0u) + (target2 >= cB2 ? 1u : 0u) +
-                                         (target2 >= cC2 ? 1u : 0u);
-                    if (ch2 & 1u) {
-                        go = false;
-                        return;
-                    }
-                    const double tau2 = div_in_range(softlog, a02);
-                    spares_update(0u, wz, ww, sp0, sp1, nsp);
-                    nm = nm + (ch2 == 0u ? 1u : 0u) - (ch2 == 2u ? 1u : 0u);
-                    n_dm += ch2 == 2u ? 1u : 0u;
-                    e += 1;
-                    if (f32t)
-                        t32 = t32 + (float)tau2;
-                    else
-                        t = t + tau2;
-                    if (hash_on) h = (h ^ (uint64_t)ch2) * kFnvPrime;
+                // One paired step: events e and e + 1 of the owner, branch-free. Both events' propensities,
+                // stop tests and channels are formed from the state as it would be after e (e + 1 reads n-
+                // after e's channel and the time after e's step), and each is committed by a select: e when it
+                // is an N- event that passes the stop tests, e + 1 when e was committed and e + 1 passes too;
+                // the first event not committed ends the lane's fast-forward, untouched, as in the unpaired
+                // loop (the full event below draws it). Straight-line code lets e's division overlap e + 1's
+                // channel (the lone wave's dependency chain is the cost here), and the next step's Philox
+                // blocks and soft logs are formed ahead, while this step's chain runs (used only if both
+                // events commit; otherwise the lane has left).
+                // (one Philox instruction stream for both halves: the counter and the round-0 words are selected
+                // per lane; two philox_event calls under a per-lane select would run both streams on every lane)
+                const auto step_words = [&](uint32_t e_own) {
+                    const uint32_t eo = __builtin_amdgcn_permlane32_swap(e_own, e_own, false, false)[0];
+                    return philox_event(helper ? eo + 1u : e_own, hp, rk);
                 };
+                uint4 wb = step_words(e);
+                double lg = softlog_neg(wb.x, logtab);
 #pragma unroll 1
                 for (uint32_t q = 0; q < kFfMax; q += 2) {
                     if ((uint32_t)__builtin_popcountll(__ballot(go)) * 8u < n_in * ECDNA_FF_STAY8) break;  // (uniform)
-                    const uint32_t eo = __builtin_amdgcn_permlane32_swap(e, e, false, false)[0];
-                    const uint4 wb = helper ? philox_event(eo + 1u, hp, rk) : philox_event(e, pre, rk);
-                    const double lg = softlog_neg(wb.x, logtab);
+                    CYC_ADD(5, 1);
+                    // the helper's block and soft log (event e + 1) to the owner
                     const uint64_t lgb = (uint64_t)__double_as_longlong(lg);
                     const uint32_t lo2 = __builtin_amdgcn_permlane32_swap((uint32_t)lgb, (uint32_t)lgb, false, false)[1];
                     const uint32_t hi2 =
@@ -1021,14 +1049,65 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     const uint32_t y2 = __builtin_amdgcn_permlane32_swap(wb.y, wb.y, false, false)[1];
                     const uint32_t z2 = __builtin_amdgcn_permlane32_swap(wb.z, wb.z, false, false)[1];
                     const uint32_t w2 = __builtin_amdgcn_permlane32_swap(wb.w, wb.w, false, false)[1];
-                    if (go) ff_event(wb.y, wb.z, wb.w, lg);
-                    if (go) ff_event(y2, z2, w2, __longlong_as_double((long long)(((uint64_t)hi2 << 32) | lo2)));
+                    const double lg2 = __longlong_as_double((long long)(((uint64_t)hi2 << 32) | lo2));
+                    const uint4 wa = wb;
+                    const double lga = lg;
+                    // the next step's words (events e + 2, e + 3), off this step's chain
+                    wb = step_words(e + 2u);
+                    lg = softlog_neg(wb.x, logtab);
+                    // event e
+                    const double fmA = (double)nm;
+                    const double cAA = rb0 * fmA;
+                    const double cBA = cAA + pbf;
+                    const double cCA = cBA + rd0 * fmA;
+                    const double a0A = cCA + pdf;
+                    const bool overA = f32t ? (t32 >= a.max_time32) : (t >= a.max_time);
+                    const double targetA = fma3((double)wa.y, 0x1p-32, 0x1p-33) * a0A;
+                    const uint32_t chA = (targetA >= cAA ? 1u : 0u) + (targetA >= cBA ? 1u : 0u) +
+                                         (targetA >= cCA ? 1u : 0u);
+                    const bool okA = go && !((e >= a.max_iter) || nm + npf >= stop32 || overA || !(a0A > 0.0)) &&
+                                     !(chA & 1u);
+                    const uint32_t nmB = nm + (chA == 0u ? 1u : 0u) - (chA == 2u ? 1u : 0u);
+                    const double tauA = div_in_range(lga, a0A);
+                    const double tB = t + tauA;
+                    const float t32B = t32 + (float)tauA;
+                    // event e + 1, from the state after e
+                    const double fmB = (double)nmB;
+                    const double cAB = rb0 * fmB;
+                    const double cBB = cAB + pbf;
+                    const double cCB = cBB + rd0 * fmB;
+                    const double a0B = cCB + pdf;
+                    const bool overB = f32t ? (t32B >= a.max_time32) : (tB >= a.max_time);
+                    const double targetB = fma3((double)y2, 0x1p-32, 0x1p-33) * a0B;
+                    const uint32_t chB = (targetB >= cAB ? 1u : 0u) + (targetB >= cBB ? 1u : 0u) +
+                                         (targetB >= cCB ? 1u : 0u);
+                    const bool okB = okA && !((e + 1u >= a.max_iter) || nmB + npf >= stop32 || overB ||
+                                              !(a0B > 0.0)) && !(chB & 1u);
+                    const uint32_t nmC = nmB + (chB == 0u ? 1u : 0u) - (chB == 2u ? 1u : 0u);
+                    const double tauB = div_in_range(lg2, a0B);
+                    // commit
+                    if (okA) spares_update(0u, wa.z, wa.w, sp0, sp1, nsp);
+                    if (okB) spares_update(0u, z2, w2, sp0, sp1, nsp);
+                    nm = okB ? nmC : (okA ? nmB : nm);
+                    n_dm += (okA && chA == 2u ? 1u : 0u) + (okB && chB == 2u ? 1u : 0u);
+                    e += (okA ? 1u : 0u) + (okB ? 1u : 0u);
+                    if (f32t)
+                        t32 = okB ? t32B + (float)tauB : (okA ? t32B : t32);
+                    else
+                        t = okB ? tB + tauB : (okA ? tB : t);
+                    if (hash_on) {
+                        const uint64_t hA = (h ^ (uint64_t)chA) * kFnvPrime;
+                        const uint64_t hB = (hA ^ (uint64_t)chB) * kFnvPrime;
+                        h = okB ? hB : (okA ? hA : h);
+                    }
+                    go = okB;
                 }
             } else if (ff_mode) {
                 bool go = active;
 #pragma unroll 1
                 for (uint32_t q = 0; q < kFfMax; ++q) {
                     if ((uint32_t)__builtin_popcountll(__ballot(go)) * 8u < n_in * ECDNA_FF_STAY8) break;  // (uniform)
+                    CYC_ADD(5, 1);
                     if (go) {
                         const double fm2 = (double)nm;
                         const double cA2 = rb0 * fm2;
@@ -1062,6 +1141,8 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                 }
             }
         }
+        CYC_MARK(1);
+        CYC_ADD(6, __builtin_popcountll(__ballot(active)));
         if (!active) continue;  // (an empty initial distribution)
         PATH_STAT(0);
         PATH_STAT_LANES(1);
@@ -1257,6 +1338,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
         }
     }
     PATH_STATS_FLUSH();
+    CYC_FLUSH();
 #ifdef ECDNA_ROT_STATS
     if ((threadIdx.x & 63u) == 0u) {
         ROT_STAT(8, c_tick);
@@ -1547,6 +1629,19 @@ extern "C" int ecdna_dev_path_stats(unsigned long long* out) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ecdna::g_path_stats), sizeof(ecdna::g_path_stats)) != hipSuccess) return -1;
     unsigned long long z[8] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(ecdna::g_path_stats), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
+#ifdef ECDNA_CYCLE_STATS
+// Development: read (and reset) the loop-section cycle counters of the last launches (tools/cycle_stats.py);
+// the max-ILP build's kernels count into their own copy
+#ifdef ECDNA_ILP_BUILD
+extern "C" int ecdna_dev_cycle_stats_ilp(unsigned long long* out) {
+#else
+extern "C" int ecdna_dev_cycle_stats(unsigned long long* out) {
+#endif
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ecdna::ECDNA_CYC_SYM), sizeof(ecdna::ECDNA_CYC_SYM)) != hipSuccess) return -1;
+    unsigned long long z[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(ecdna::ECDNA_CYC_SYM), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif
 #if defined(ECDNA_ROT_STATS) && !defined(ECDNA_ILP_BUILD)
