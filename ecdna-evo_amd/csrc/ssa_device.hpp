@@ -126,21 +126,38 @@ __device__ __forceinline__ uint64_t mul_u32_wide(uint32_t a, uint32_t b) {
     return d;
 }
 
-__device__ __forceinline__ double softlog_neg(uint32_t w, const double2* tab) {
+// softlog_neg in two halves: the table load (begin) and the arithmetic after it (end), so that a loop can
+// issue the load one iteration ahead and overlap its latency
+struct SoftlogParts {
+    double2 cl;
+    double m;
+    int ex;
+};
+
+__device__ __forceinline__ SoftlogParts softlog_begin(uint32_t w, const double2* tab) {
     const double d = (double)w + 0.5;  // exact
     const uint64_t bits = (uint64_t)__double_as_longlong(d);
     const uint32_t hi = (uint32_t)(bits >> 32);
-    const int ex = (int)(hi >> 20) - 1022;
-    const double m = __longlong_as_double((long long)((bits & 0x000fffffffffffffull) | (1022ull << 52)));
-    const double2 cl = tab[(hi >> 13) & 127u];
-    const double r = m * cl.x - 1.0;
+    SoftlogParts p;
+    p.ex = (int)(hi >> 20) - 1022;
+    p.m = __longlong_as_double((long long)((bits & 0x000fffffffffffffull) | (1022ull << 52)));
+    p.cl = tab[(hi >> 13) & 127u];
+    return p;
+}
+
+__device__ __forceinline__ double softlog_end(const SoftlogParts& p) {
+    const double r = p.m * p.cl.x - 1.0;
     double q = fma3(r, 0x1.2492492492492p-3, -0x1.5555555555555p-3);  // 1/7, -1/6
     q = fma3(r, q, 0x1.999999999999ap-3);                                // 1/5
     q = fma3(r, q, -0x1p-2);                                             // -1/4
     q = fma3(r, q, 0x1.5555555555555p-2);                                // 1/3
     q = fma3(r, q, -0x1p-1);                                             // -1/2
     const double l = fma(r * r, q, r);                                  // ln(1 + r)
-    return -fma((double)(ex - 32), 0x1.62e42fefa39efp-1, cl.y + l);
+    return -fma((double)(p.ex - 32), 0x1.62e42fefa39efp-1, p.cl.y + l);
+}
+
+__device__ __forceinline__ double softlog_neg(uint32_t w, const double2* tab) {
+    return softlog_end(softlog_begin(w, tab));
 }
 
 // n / d, the correctly rounded IEEE quotient (the oracle's C division), for operands in the stepper's

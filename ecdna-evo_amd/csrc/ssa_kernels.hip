@@ -1036,11 +1036,12 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     return philox_event(helper ? eo + 1u : e_own, hp, rk);
                 };
                 uint4 wb = step_words(e);
-                double lg = softlog_neg(wb.x, logtab);
+                SoftlogParts lp = softlog_begin(wb.x, logtab);  // (finished at the top of the step that uses it)
 #pragma unroll 1
                 for (uint32_t q = 0; q < kFfMax; q += 2) {
                     if ((uint32_t)__builtin_popcountll(__ballot(go)) * 8u < n_in * ECDNA_FF_STAY8) break;  // (uniform)
                     CYC_ADD(5, 1);
+                    const double lg = softlog_end(lp);
                     // the helper's block and soft log (event e + 1) to the owner
                     const uint64_t lgb = (uint64_t)__double_as_longlong(lg);
                     const uint32_t lo2 = __builtin_amdgcn_permlane32_swap((uint32_t)lgb, (uint32_t)lgb, false, false)[1];
@@ -1054,20 +1055,21 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     const double lga = lg;
                     // the next step's words (events e + 2, e + 3), off this step's chain
                     wb = step_words(e + 2u);
-                    lg = softlog_neg(wb.x, logtab);
-                    // event e
+                    lp = softlog_begin(wb.x, logtab);
+                    // event e (conditions as 0/1 words combined with bitwise ops: no short-circuit branches, so
+                    // the step stays one basic block for the scheduler)
                     const double fmA = (double)nm;
                     const double cAA = rb0 * fmA;
                     const double cBA = cAA + pbf;
                     const double cCA = cBA + rd0 * fmA;
                     const double a0A = cCA + pdf;
-                    const bool overA = f32t ? (t32 >= a.max_time32) : (t >= a.max_time);
+                    const uint32_t overA = f32t ? (uint32_t)(t32 >= a.max_time32) : (uint32_t)(t >= a.max_time);
                     const double targetA = fma3((double)wa.y, 0x1p-32, 0x1p-33) * a0A;
-                    const uint32_t chA = (targetA >= cAA ? 1u : 0u) + (targetA >= cBA ? 1u : 0u) +
-                                         (targetA >= cCA ? 1u : 0u);
-                    const bool okA = go && !((e >= a.max_iter) || nm + npf >= stop32 || overA || !(a0A > 0.0)) &&
-                                     !(chA & 1u);
-                    const uint32_t nmB = nm + (chA == 0u ? 1u : 0u) - (chA == 2u ? 1u : 0u);
+                    const uint32_t chA = (uint32_t)(targetA >= cAA) + (uint32_t)(targetA >= cBA) +
+                                         (uint32_t)(targetA >= cCA);
+                    const uint32_t okA = (uint32_t)go & (uint32_t)(e < a.max_iter) & (uint32_t)(nm + npf < stop32) &
+                                         (overA ^ 1u) & (uint32_t)(a0A > 0.0) & (~chA & 1u);
+                    const uint32_t nmB = nm + (uint32_t)(chA == 0u) - (uint32_t)(chA == 2u);
                     const double tauA = div_in_range(lga, a0A);
                     const double tB = t + tauA;
                     const float t32B = t32 + (float)tauA;
@@ -1077,30 +1079,33 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     const double cBB = cAB + pbf;
                     const double cCB = cBB + rd0 * fmB;
                     const double a0B = cCB + pdf;
-                    const bool overB = f32t ? (t32B >= a.max_time32) : (tB >= a.max_time);
+                    const uint32_t overB = f32t ? (uint32_t)(t32B >= a.max_time32) : (uint32_t)(tB >= a.max_time);
                     const double targetB = fma3((double)y2, 0x1p-32, 0x1p-33) * a0B;
-                    const uint32_t chB = (targetB >= cAB ? 1u : 0u) + (targetB >= cBB ? 1u : 0u) +
-                                         (targetB >= cCB ? 1u : 0u);
-                    const bool okB = okA && !((e + 1u >= a.max_iter) || nmB + npf >= stop32 || overB ||
-                                              !(a0B > 0.0)) && !(chB & 1u);
-                    const uint32_t nmC = nmB + (chB == 0u ? 1u : 0u) - (chB == 2u ? 1u : 0u);
+                    const uint32_t chB = (uint32_t)(targetB >= cAB) + (uint32_t)(targetB >= cBB) +
+                                         (uint32_t)(targetB >= cCB);
+                    const uint32_t okB = okA & (uint32_t)(e + 1u < a.max_iter) & (uint32_t)(nmB + npf < stop32) &
+                                         (overB ^ 1u) & (uint32_t)(a0B > 0.0) & (~chB & 1u);
+                    const uint32_t nmC = nmB + (uint32_t)(chB == 0u) - (uint32_t)(chB == 2u);
                     const double tauB = div_in_range(lg2, a0B);
-                    // commit
-                    if (okA) spares_update(0u, wa.z, wa.w, sp0, sp1, nsp);
-                    if (okB) spares_update(0u, z2, w2, sp0, sp1, nsp);
-                    nm = okB ? nmC : (okA ? nmB : nm);
-                    n_dm += (okA && chA == 2u ? 1u : 0u) + (okB && chB == 2u ? 1u : 0u);
-                    e += (okA ? 1u : 0u) + (okB ? 1u : 0u);
+                    // commit. An N- event consumes no stream word after w1, so its spare update pushes w2 and
+                    // w3 onto the stack and leaves exactly those two (spares_update with used = 0).
+                    const bool cA = okA != 0u, cB = okB != 0u;
+                    sp0 = cB ? w2 : (cA ? wa.w : sp0);
+                    sp1 = cB ? z2 : (cA ? wa.z : sp1);
+                    nsp = cA ? 2u : nsp;
+                    nm = cB ? nmC : (cA ? nmB : nm);
+                    n_dm += (okA & (uint32_t)(chA == 2u)) + (okB & (uint32_t)(chB == 2u));
+                    e += okA + okB;
                     if (f32t)
-                        t32 = okB ? t32B + (float)tauB : (okA ? t32B : t32);
+                        t32 = cB ? t32B + (float)tauB : (cA ? t32B : t32);
                     else
-                        t = okB ? tB + tauB : (okA ? tB : t);
+                        t = cB ? tB + tauB : (cA ? tB : t);
                     if (hash_on) {
                         const uint64_t hA = (h ^ (uint64_t)chA) * kFnvPrime;
                         const uint64_t hB = (hA ^ (uint64_t)chB) * kFnvPrime;
-                        h = okB ? hB : (okA ? hA : h);
+                        h = cB ? hB : (cA ? hA : h);
                     }
-                    go = okB;
+                    go = cB;
                 }
             } else if (ff_mode) {
                 bool go = active;
