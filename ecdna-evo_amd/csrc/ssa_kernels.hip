@@ -482,16 +482,20 @@ ECDNA_DEV_STATIC __device__ unsigned long long g_path_stats[8];
 // tools/cycle_stats.py), per wave, summed over waves: [0] shader-clock cycles from the loop top through the
 // replicate boundary, [1] the fast-forward block (entry test included), [2] the full event and the loop
 // latch, [3] iterations, [4] fast-forward entries, [5] fast-forward steps, [6] lanes entering the full event,
-// [7] whole-kernel cycles. Marks sit at wave-uniform points; the wave's lane 0 flushes.
+// [7] whole-kernel cycles; inside the full event (lanes past the stop test) [8] propensities and stop test,
+// [9] Philox block and channel, [10] cell pick, [11] segregation, [12] error and capacity checks, [13] time
+// step, [14] counter and large-k row updates ([2] then holds the commit and the loop latch). Marks sit at
+// wave-uniform points of their region (a mark waits for the wave's LDS operations: a rough attribution);
+// the wave's lane 0 flushes.
 #ifdef ECDNA_CYCLE_STATS
 #ifdef ECDNA_ILP_BUILD
 #define ECDNA_CYC_SYM g_cycle_stats_ilp
 #else
 #define ECDNA_CYC_SYM g_cycle_stats
 #endif
-ECDNA_DEV_STATIC __device__ unsigned long long ECDNA_CYC_SYM[8];
+ECDNA_DEV_STATIC __device__ unsigned long long ECDNA_CYC_SYM[16];
 #define CYC_DECL                                                                                               \
-    unsigned long long cy_[8] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull};                              \
+    unsigned long long cy_[16] = {};                                                                           \
     const unsigned long long cy_start_ = clock64();                                                           \
     unsigned long long cy_t_ = cy_start_
 #define CYC_MARK(i)                                                                                            \
@@ -505,7 +509,7 @@ ECDNA_DEV_STATIC __device__ unsigned long long ECDNA_CYC_SYM[8];
     do {                                                                                                       \
         cy_[7] = clock64() - cy_start_;                                                                        \
         if ((threadIdx.x & 63u) == 0u)                                                                         \
-            for (int q = 0; q < 8; ++q)                                                                        \
+            for (int q = 0; q < 16; ++q)                                                                       \
                 __hip_atomic_fetch_add(&ECDNA_CYC_SYM[q], cy_[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   \
     } while (0)
 #else
@@ -1025,17 +1029,17 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                 // after e's channel and the time after e's step), and each is committed by a select: e when it
                 // is an N- event that passes the stop tests, e + 1 when e was committed and e + 1 passes too;
                 // the first event not committed ends the lane's fast-forward, untouched, as in the unpaired
-                // loop (the full event below draws it). Straight-line code lets e's division overlap e + 1's
-                // channel (the lone wave's dependency chain is the cost here), and the next step's Philox
-                // blocks and soft logs are formed ahead, while this step's chain runs (used only if both
-                // events commit; otherwise the lane has left).
+                // loop (the full event below draws it). The step is one basic block, and the next step's Philox
+                // blocks and soft-log table loads are issued ahead, while this step's events run (used only if
+                // both events commit; otherwise the lane has left). A lone wave pays roughly its instruction
+                // count here (forming e + 1 for both possible n- alongside e, to cut the chain, was slower).
                 // (one Philox instruction stream for both halves: the counter and the round-0 words are selected
                 // per lane; two philox_event calls under a per-lane select would run both streams on every lane)
-                const auto step_words = [&](uint32_t e_own) {
-                    const uint32_t eo = __builtin_amdgcn_permlane32_swap(e_own, e_own, false, false)[0];
-                    return philox_event(helper ? eo + 1u : e_own, hp, rk);
-                };
-                uint4 wb = step_words(e);
+                // ctr: the lane's event counter, e for an owner and its owner's e + 1 for a helper; a step that
+                // continues advances both by 2 (a lane that commits fewer leaves, and its next words go unused)
+                uint32_t ctr = __builtin_amdgcn_permlane32_swap(e, e, false, false)[0] + 1u;
+                ctr = helper ? ctr : e;
+                uint4 wb = philox_event(ctr, hp, rk);
                 SoftlogParts lp = softlog_begin(wb.x, logtab);  // (finished at the top of the step that uses it)
 #pragma unroll 1
                 for (uint32_t q = 0; q < kFfMax; q += 2) {
@@ -1054,7 +1058,8 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     const uint4 wa = wb;
                     const double lga = lg;
                     // the next step's words (events e + 2, e + 3), off this step's chain
-                    wb = step_words(e + 2u);
+                    ctr += 2u;
+                    wb = philox_event(ctr, hp, rk);
                     lp = softlog_begin(wb.x, logtab);
                     // event e (conditions as 0/1 words combined with bitwise ops: no short-circuit branches, so
                     // the step stays one basic block for the scheduler)
@@ -1189,6 +1194,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                 }
             }
 
+            CYC_MARK(8);
             const uint32_t rid_lo = (uint32_t)rid, rid_hi = (uint32_t)(rid >> 32);
             const uint4 w = philox_event(e, pre, rk);
             // direct method: the channel is the number of cumulative propensities <= target (the first i
@@ -1200,6 +1206,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
             const bool nplus_ev = (ch & 1u) != 0;  // ProliferateNPlus or DeathNPlus: a cell is picked
             const bool prolif = ch == 1u;
 
+            CYC_MARK(9);
             WordStream ws;
             ws.w2 = w.z;
             ws.w3 = w.w;
@@ -1229,6 +1236,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                 k = gload_u16_l2(row + (idx - ns));
             }
 
+            CYC_MARK(10);
             // Exponential::increase_nplus (src/proliferation.rs:25-111): its draws and error checks
             const uint32_t n = 2u * k;
             uint32_t k1v = k;
@@ -1268,6 +1276,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                 if (SEG != ECDNA_SEG_BINOMIAL_NO_UNEVEN)
                     un = (k1v == 0u || k1v == n) ? (SEG == ECDNA_SEG_BINOMIAL_NO_NMINUS ? 2u : 1u) : 0u;
             }
+            CYC_MARK(11);
             // checked_mul panic (src/proliferation.rs:63-67)
             ev_err = (k > 32767u) ? (uint32_t)ECDNA_REP_ERR_OVERFLOW : ev_err;
             // daughters (none for a death): [k1, k2] on an even split, [n] on an uneven one
@@ -1287,12 +1296,14 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                 if (prolif && ev_err == 0u && ((has_a && !sa) || (has_b && !sb)) && nb_new > ra->big_cap)
                     ev_err = ECDNA_REP_ERR_CELL_CAP;
             }
+            CYC_MARK(12);
             if (prolif && ev_err) {  // the event is not applied; the replicate stops (rare)
                 err = ev_err;
                 stop = ECDNA_STOP_ERROR;
                 active = false;
             } else {
                 const double tau = div_in_range(softlog_neg(w.x, logtab), a0);
+                CYC_MARK(13);
 
                 const uint32_t ns_old = ns;
                 // common case: every copy number involved is binned -> LDS only, no branch
@@ -1325,6 +1336,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                         nb -= 1;
                     }
                 }
+                CYC_MARK(14);
                 spares_update(nplus_ev ? ws.pos : 0u, w.z, w.w, sp0, sp1, nsp);
                 nm = nm + ((ch == 0u || (prolif && un == 1u)) ? 1u : 0u) - ((BD && ch == 2u) ? 1u : 0u);
                 n_un += (prolif && un != 0u) ? 1u : 0u;
@@ -1645,7 +1657,7 @@ extern "C" int ecdna_dev_cycle_stats_ilp(unsigned long long* out) {
 extern "C" int ecdna_dev_cycle_stats(unsigned long long* out) {
 #endif
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ecdna::ECDNA_CYC_SYM), sizeof(ecdna::ECDNA_CYC_SYM)) != hipSuccess) return -1;
-    unsigned long long z[8] = {};
+    unsigned long long z[16] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(ecdna::ECDNA_CYC_SYM), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

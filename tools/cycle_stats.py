@@ -1,7 +1,7 @@
 """Loop-section cycle counters of the bin stepper over one launch (development tool): where a wave's time
 goes (replicate boundary, N- fast-forward, full event), per wave-iteration and per event. Needs a library
 built with -DECDNA_CYCLE_STATS (EXTRA=-DECDNA_CYCLE_STATS bash tools/ab_build.sh WORKTREE cyc), selected
-with ECDNA_SSA_LIB. Usage: python tools/cycle_stats.py [c2|c3|c4|c5] (C4 and C5: the 8-GPU rank-0 shard)"""
+with ECDNA_SSA_LIB. Usage: [PROBE_KMAX=K] python tools/cycle_stats.py [c2|c3|c4|c5] (C4 and C5: the 8-GPU rank-0 shard)"""
 import ctypes as C
 import dataclasses
 import json
@@ -15,13 +15,15 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import probe_configs  # noqa: E402
 
 KMAX = {"c2": 32, "c3": 32, "c4": 64, "c5": 64}
-NAMES = ["cyc_boundary", "cyc_ff", "cyc_full", "iters", "ff_entries", "ff_steps", "full_lanes", "cyc_kernel"]
+NAMES = ["cyc_boundary", "cyc_ff", "cyc_full", "iters", "ff_entries", "ff_steps", "full_lanes", "cyc_kernel",
+         "f_prop_stop", "f_philox_channel", "f_pick", "f_segregation", "f_checks", "f_time_step", "f_updates"]
 
 
 def main():
     name = sys.argv[1] if len(sys.argv) > 1 else "c5"
     spec = probe_configs.CONFIGS[name](0, 8) if name in ("c4", "c5") else probe_configs.CONFIGS[name]()
-    spec = dataclasses.replace(spec, flags=abi.FLAG_BIN_STORE, bin_kmax=KMAX[name], _keep=[])
+    kmax = int(os.environ.get("PROBE_KMAX", KMAX[name]))
+    spec = dataclasses.replace(spec, flags=abi.FLAG_BIN_STORE, bin_kmax=kmax, _keep=[])
     lib = engine.lib()
     readers = []
     for sym in ("ecdna_dev_cycle_stats", "ecdna_dev_cycle_stats_ilp"):
@@ -29,12 +31,12 @@ def main():
         fn.argtypes = [C.POINTER(C.c_ulonglong)]
         readers.append(fn)
     ctx = engine.Context(spec)
-    buf = (C.c_ulonglong * 8)()
+    buf = (C.c_ulonglong * 16)()
     for fn in readers:
         fn(buf)
     ctx.launch()
     ms, _ = ctx.sync()
-    tot = [0] * 8
+    tot = [0] * 16
     for fn in readers:
         fn(buf)
         tot = [a + int(b) for a, b in zip(tot, buf)]
@@ -43,7 +45,7 @@ def main():
     it = max(d["iters"], 1)
     cyc = d["cyc_boundary"] + d["cyc_ff"] + d["cyc_full"]
     print(json.dumps({"config": name, "ms": ms, "events": ev, "geometry": ctx.geometry(), **d,
-                      "per_iter": {k: round(d[k] / it, 2) for k in NAMES[:3] + NAMES[4:7]},
+                      "per_iter": {k: round(d[k] / it, 2) for k in NAMES[:3] + NAMES[4:7] + NAMES[8:]},
                       "share": {k: round(d[k] / max(cyc, 1), 3) for k in NAMES[:3]},
                       "ff_steps_per_entry": round(d["ff_steps"] / max(d["ff_entries"], 1), 2)}), flush=True)
     ctx.close()
