@@ -35,6 +35,7 @@ Extra JSON fields:
                   BTPE, "port") on a bounded sample of the same workload, rank 0 at N=1 only.
 """
 import argparse
+import dataclasses
 import json
 import os
 import sys
@@ -270,6 +271,9 @@ def main():
     ap.add_argument("--total", type=int, default=None,
                     help="rehearsal only: replicates in total for the strong-scaling workloads (c2/c4/c5)")
     ap.add_argument("--max-cells", type=int, default=None, help="rehearsal only: override the workload's cell cap")
+    ap.add_argument("--draws", choices=("philox", "reference"), default="philox",
+                    help="reference: the Rust reference's own draws seed for seed (ECDNA_FLAG_REFERENCE_DRAWS, "
+                         "DESIGN.md §4.1; row store only): the seed-for-seed mode's throughput, not the metric's")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -301,8 +305,13 @@ def main():
         total = args.total or WORKLOADS[args.workload][0]
         first, n, stride = shard.interleaved_range(rank, n_gpus, total)
         reps = n
+    refdraws = args.draws == "reference"
+    if refdraws and args.store != "rows":
+        ap.error("--draws reference runs on the row store only (--store rows)")
     spec = workload_spec(first, n, total, device=local if distributed else 0, store=args.store,
                          bin_kmax=args.bin_kmax, workload=args.workload, stride=stride, max_cells=args.max_cells)
+    if refdraws:
+        spec = dataclasses.replace(spec, flags=spec.flags | abi.FLAG_REFERENCE_DRAWS, _keep=[])
     n_sets = len(spec.rates)
     ctx = engine.Context(spec)
     hist = torch.zeros(n_sets * spec.hist_bins, dtype=torch.int64, device="cuda")
@@ -368,7 +377,7 @@ def main():
     if rank == 0:
         avg_kernel_s = sum(kernel_ms) / len(kernel_ms) * 1e-3
         achieved = local_alg / avg_kernel_s / 1e9
-        pmc = load_pmc(args.store) if weak else {}  # (the committed PMC summaries are C3's)
+        pmc = load_pmc(args.store) if weak and not refdraws else {}  # (the committed PMC summaries: C3, philox)
         traffic = pmc.get("hbm_bytes_per_launch")
         kernel_eps = local_events / avg_kernel_s
         transactions = None
@@ -419,7 +428,9 @@ def main():
             "higher_is_better": True,
             "scaling": "weak" if weak else "strong",
             "vs_baseline": None,
-            "dtype": "u16+f64",
+            "dtype": "u16+f32" if refdraws else "u16+f64",
+            "draws": "reference (ChaCha8 seed*10+i, first-reaction, BINV/BTPE, f32 time; seed for seed)"
+                     if refdraws else "philox (the engine's draw mapping, DESIGN.md §3)",
             "store": args.store,
             "data": "synthetic",
             "config": {
@@ -443,7 +454,7 @@ def main():
                 # and registers), HBM request rate for the row store; achieved / peak / frac below are the
                 # contract's nominal HBM view (SURVEY.md §8d algorithmic bytes of the reference's u16-row
                 # representation over the kernel's duration, vs 8 TB/s), which neither store is bound by
-                "bound": "valu_issue" if args.store == "bins" else "hbm_requests",
+                "bound": "divergent_samplers" if refdraws else ("valu_issue" if args.store == "bins" else "hbm_requests"),
                 "issue_frac": issue["frac"] if issue else None,
                 "frac_kind": "nominal_hbm_algorithmic_bytes",
                 "achieved": achieved,
