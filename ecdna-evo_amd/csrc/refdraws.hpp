@@ -128,6 +128,33 @@ __device__ __forceinline__ double exp_cr(double y, const double* cexp) {
     return __builtin_ldexp(v.hi + v.lo, (int)qq);
 }
 
+// e^y for -22 <= y <= 0 in plain double arithmetic (the 2^(j/64) table head and a degree-6 polynomial):
+// within about 2^-49 of e^y, relative (the head's rounding, r's reduction, six Horner roundings, the final
+// product); not correctly rounded, so only used to decide comparisons against exp_cr clear of the boundary
+__device__ __forceinline__ double exp_approx(double y, const double* cexp) {
+    const double kd = __builtin_rint(y * ECDNA_CEXP_INV_L);
+    const int64_t k = (int64_t)kd;
+    const double r = (y - kd * ECDNA_CEXP_L_HI) - kd * ECDNA_CEXP_L_LO;
+    double q = __builtin_fma(r, 1.0 / 720.0, 1.0 / 120.0);
+    q = __builtin_fma(r, q, 1.0 / 24.0);
+    q = __builtin_fma(r, q, 1.0 / 6.0);
+    q = __builtin_fma(r, q, 0.5);
+    q = __builtin_fma(r, q, 1.0);
+    q = __builtin_fma(r, q, 1.0);
+    const int64_t jj = k & 63, qq = (k - jj) / 64;
+    return __builtin_ldexp(cexp[2 * jj] * q, (int)qq);
+}
+
+// lhs < exp_cr(y) for -22 <= y <= 0, the same result: exp_approx decides whenever lhs is further than
+// 2^-40 (relative) from it, far beyond both functions' errors (exp_cr is within 2^-53 of e^y); otherwise
+// the correctly rounded value does (about once in 2^40 comparisons)
+__device__ __forceinline__ bool lt_exp_cr(double lhs, double y, const double* cexp) {
+    const double a = exp_approx(y, cexp);
+    if (lhs < a * (1.0 - 0x1p-40)) return true;
+    if (lhs > a * (1.0 + 0x1p-40)) return false;
+    return lhs < exp_cr(y, cexp);
+}
+
 // Rust's `f as i64`: saturating, NaN -> 0
 __device__ __forceinline__ int64_t f64_to_i64(double x) {
     if (x != x) return 0;
@@ -157,16 +184,25 @@ __device__ __forceinline__ double float_1_2(uint64_t bits) {
     b = __builtin_rotateleft32(b, 7);
 
 // The per-lane generator: key (uniform, 8 words from the host's seed_from_u64), 64-bit block counter and
-// stream, and the current block's 16 words in LDS ([word][lane]: a wave's accesses hit distinct banks).
+// stream, and a ring of two 16-word blocks per lane in LDS ([word][lane]: a wave's accesses hit distinct
+// banks). Words come out in stream order whatever the refill timing. Lanes consume words at different
+// rates, so a refill inside next_u32 would run (masked) for the whole wave at nearly every draw site;
+// instead top_up(), called once per event at a wave-uniform point, generates the next block for lanes with
+// fewer than 16 words buffered, and next_u32 refills on demand only when a lane's event outruns that (rare
+// rejection loops).
 struct ChaCha8 {
     const uint32_t* key;   // 8 words
-    uint32_t* buf;         // LDS, word w of this lane at buf[w * stride]
+    uint32_t* buf;         // LDS, ring word w (0..31) of this lane at buf[w * stride]
     uint32_t stride;
     uint64_t counter;      // next block
     uint32_t s_lo, s_hi;   // stream
-    uint32_t pos;          // words of the current block used (16 = empty)
+    uint32_t head, tail;   // words read / generated (tail - head = buffered, 0..32)
 
-    __device__ __forceinline__ void refill() {
+    __device__ __forceinline__ void reset() {
+        counter = 0;
+        head = tail = 0;
+    }
+    __device__ __forceinline__ void refill() {  // one block into ring words tail .. tail + 15 (mod 32)
         uint32_t in[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
                            key[0], key[1], key[2], key[3], key[4], key[5], key[6], key[7],
                            (uint32_t)counter, (uint32_t)(counter >> 32), s_lo, s_hi};
@@ -184,14 +220,18 @@ struct ChaCha8 {
             ECDNA_QR(x[2], x[7], x[8], x[13]);
             ECDNA_QR(x[3], x[4], x[9], x[14]);
         }
+        uint32_t* const dst = buf + (tail & 16u) * stride;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) buf[i * stride] = x[i] + in[i];
+        for (int i = 0; i < 16; ++i) dst[i * stride] = x[i] + in[i];
         counter += 1;
-        pos = 0;
+        tail += 16u;
+    }
+    __device__ __forceinline__ void top_up() {
+        if (tail - head < 16u) refill();
     }
     __device__ __forceinline__ uint32_t next_u32() {
-        if (pos >= 16u) refill();
-        return buf[(pos++) * stride];
+        if (head == tail) refill();
+        return buf[(head++ & 31u) * stride];
     }
     __device__ __forceinline__ uint64_t next_u64() {
         const uint32_t lo = next_u32();
@@ -223,7 +263,8 @@ __device__ __forceinline__ double exp1(ChaCha8& rng, const double* zx, const dou
         const double x = u * zx[i];
         if (x < zx[i + 1]) return x;
         if (i == 0) return ECDNA_ZIG_EXP_R - log_cr(rng.gen_f64(), clog);
-        if (zf[i + 1] + (zf[i] - zf[i + 1]) * rng.gen_f64() < exp_cr(-x, cexp)) return x;
+        // (the wedge test against the correctly rounded e^-x, decided by lt_exp_cr's filter; x < R < 22)
+        if (lt_exp_cr(zf[i + 1] + (zf[i] - zf[i + 1]) * rng.gen_f64(), -x, cexp)) return x;
     }
 }
 

@@ -86,6 +86,8 @@ def lib():
     L.oracle_compat_log.restype = C.c_double
     L.oracle_compat_exp.argtypes = [C.c_double]
     L.oracle_compat_exp.restype = C.c_double
+    L.oracle_compat_exp_approx.argtypes = [C.c_double]
+    L.oracle_compat_exp_approx.restype = C.c_double
     _lib = L
     return L
 
@@ -226,6 +228,11 @@ def compat_log(x: float) -> float:
 
 def compat_exp(x: float) -> float:
     return lib().oracle_compat_exp(x)
+
+
+def compat_exp_approx(x: float) -> float:
+    """csrc/refdraws.hpp exp_approx restated (the wedge-test filter; tests only)."""
+    return lib().oracle_compat_exp_approx(x)
 
 
 def chacha_block(state, rounds: int):

@@ -319,6 +319,23 @@ static double exp1(oracle_chacha* r) {
 }
 double oracle_compat_exp1(oracle_chacha* r) { return exp1(r); }
 
+/* csrc/refdraws.hpp exp_approx, the same operations: the GPU's plain-double e^y (-22 <= y <= 0) that decides
+ * the ziggurat's wedge comparisons clear of the boundary (lt_exp_cr); restated here so that a CPU test can
+ * bound its error against exact arithmetic (tests/test_compat_math.py). The compat draws never use it. */
+double oracle_compat_exp_approx(double y) {
+    const double kd = rint(y * ECDNA_CEXP_INV_L);
+    const int64_t k = (int64_t)kd;
+    const double r = (y - kd * ECDNA_CEXP_L_HI) - kd * ECDNA_CEXP_L_LO;
+    double q = fma(r, 1.0 / 720.0, 1.0 / 120.0);
+    q = fma(r, q, 1.0 / 24.0);
+    q = fma(r, q, 1.0 / 6.0);
+    q = fma(r, q, 0.5);
+    q = fma(r, q, 1.0);
+    q = fma(r, q, 1.0);
+    const int64_t jj = k & 63, qq = (k - jj) / 64;
+    return ldexp(CEXP_TAB[2 * jj] * q, (int)qq);
+}
+
 /* Rust's `f as i64`: saturating, NaN -> 0 (a C cast of an out-of-range double is undefined) */
 static inline int64_t f64_to_i64(double x) {
     if (x != x) return 0;

@@ -55,6 +55,22 @@ def test_compat_exp_is_correctly_rounded(oracle_mod):
         assert oracle_mod.compat_exp(y) == float(Decimal(y).exp()), y
 
 
+def test_exp_filter_error_bound(oracle_mod):
+    """The GPU's wedge test decides lhs < exp_cr(-x) with a plain-double e^-x whenever lhs is further than
+    2^-40 (relative) from it (csrc/refdraws.hpp lt_exp_cr); that is exact provided the plain value is within
+    2^-41 of e^y. Its restatement is within 2^-48 here, over the ziggurat's range and beyond."""
+    getcontext().prec = 60
+    rng = random.Random(9)
+    ys = [-rng.uniform(0, 7.7) for _ in range(6000)] + [-rng.uniform(0, 22) for _ in range(2000)]
+    ys += [0.0, -7.697117470131050, -1e-300, -22.0]
+    worst = 0.0
+    for y in ys:
+        exact = Decimal(y).exp()
+        err = abs((Decimal(oracle_mod.compat_exp_approx(y)) - exact) / exact)
+        worst = max(worst, float(err))
+    assert worst < 2.0 ** -48, worst
+
+
 @pytest.mark.parametrize("fn,gen", [
     ("log", lambda r: r.random() or 0.5),
     ("log", lambda r: r.uniform(0.5, 3.0)),
