@@ -650,6 +650,24 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
         atomicAdd(cnt_w + word_index(b), shifted(b, d));
         atomicAdd(sum_w + word_index(g), shifted(g, d));
     };
+    // the event's three counter updates (C32, planar, 256-lane workgroups): the copy number clamped into 1..K
+    // (one v_med3; a lane adding 0 may pass any value, and its add of 0 to some counter of its own changes
+    // nothing), the bin's byte offset kc * 1024 + 4 tid - 1024 (one v_lshl_add) and the group sum's from it,
+    // (offset >> 13) * 1024 + 4 tid, since offset >> 13 = (kc - 1) >> 3 while 4 tid < 1024: five VALU per update
+    // with the select of d, against seven for bin_add's masked indices. Same counters, same adds.
+    const uint32_t bin_c = 4u * tid - 4u * BLK, sum_c = 4u * tid;
+    auto bin_add_ev = [&](uint32_t k, uint32_t d) {
+        if (!C32 || BLK != 256) {
+            bin_add(k, d);
+            return;
+        }
+        const uint32_t kc = min(max(k, 1u), K);
+        const uint32_t off = (kc << 10) + bin_c;
+        atomicAdd(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(cnt_w) + off), d);
+        uint32_t g = off >> 13;
+        asm("" : "+v"(g));  // (keeps shift-then-v_lshl_add: the compiler would re-form it as shift, mask and add)
+        atomicAdd(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(sum_w) + ((g << 10) + sum_c)), d);
+    };
     // canonical position i -> copy number, valid for i < ns (other lanes get an unused in-range value).
     // Branch-free subtract/shift form (the compiler's compare + select form took ~40 % more VALU): with
     // d_j = i - (prefix sum through group j), the group is the number of d_j >= 0 and the offset inside
@@ -1307,10 +1325,10 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
 
                 const uint32_t ns_old = ns;
                 // common case: every copy number involved is binned -> LDS only, no branch
-                // (bin_add masks its copy number into range, so lanes adding 0 need no select)
-                bin_add(k, (nplus_ev && small) ? 0xffffffffu : 0u);
-                bin_add(da, sa ? 1u : 0u);
-                bin_add(db, sb ? 1u : 0u);
+                // (bin_add_ev clamps its copy number into range, so lanes adding 0 need no select)
+                bin_add_ev(k, (nplus_ev && small) ? 0xffffffffu : 0u);
+                bin_add_ev(da, sa ? 1u : 0u);
+                bin_add_ev(db, sb ? 1u : 0u);
                 ns = ns - ((nplus_ev && small) ? 1u : 0u) + (sa ? 1u : 0u) + (sb ? 1u : 0u);
                 if (nplus_ev && (!small || (has_a && !sa) || (has_b && !sb))) {  // the large-k row (rare)
                     PATH_STAT(6);
