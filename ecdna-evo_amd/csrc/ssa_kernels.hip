@@ -436,6 +436,10 @@ constexpr int kCpolSc1 = 16;  // buffer cache policy: sc1 (gfx940+ bit 4)
 #ifndef ECDNA_FF_ENTER8
 #define ECDNA_FF_ENTER8 7  // enter when >= this many eighths of the lanes expect an N- event w.p. >= ECDNA_FF_ENTER8 / 8
 #endif
+#ifndef ECDNA_FF_TEST_EVERY
+#define ECDNA_FF_TEST_EVERY 32u  // while a wave is not fast-forwarding, its entry test runs every this many
+                                // iterations (C3, which never enters: 8 -> 32 is -1.2 %; C4 / C5 unchanged)
+#endif
 #ifndef ECDNA_FF_STAY8
 #define ECDNA_FF_STAY8 7   // keep going while >= this many eighths of the entered lanes do
 #endif
@@ -1017,9 +1021,9 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
         // most of the wave's lanes draw N- events, they run them here, up to kFfMax per iteration, without
         // the pick, the segregation and the counter updates. A lane leaves at its first N+ event or stop
         // condition, untouched: the full event below draws that same event. Snapshots (checked per
-        // event) keep the full loop. The entry test runs every 8th iteration while the wave is not
+        // event) keep the full loop. The entry test runs every 32nd iteration (ECDNA_FF_TEST_EVERY) while the wave is not
         // fast-forwarding, every iteration while it is (wave-uniform control: ballots at the loop top).
-        if (BD && kFfMax && !a.n_snap && (ff_mode || (ff_tick & 7u) == 0u)) {
+        if (BD && kFfMax && !a.n_snap && (ff_mode || (ff_tick & (ECDNA_FF_TEST_EVERY - 1u)) == 0u)) {
             const uint32_t npf = ns + nb;  // n+ is fixed during N- events
             const double fpf = (double)npf;
             const double pbf = rb1 * fpf, pdf = rd1 * fpf;
@@ -1241,17 +1245,42 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
 
             // uniform N+ cell: Lemire multiply-shift on w2; exact rejection (rare) from the stream
             uint64_t m = mul_u32_wide(w.z, np);
-            if (nplus_ev && (uint32_t)m < np) {
-                PATH_STAT(3);
-                const uint32_t thr = (0u - np) % np;
-                while ((uint32_t)m < thr) m = (uint64_t)ws.next() * np;
-            }
-            const uint32_t idx = (uint32_t)(m >> 32);
-            const bool small = idx < ns;
-            uint32_t k = bin_find(small ? idx : 0u);
-            if (nplus_ev && !small) {  // large-k row (rare)
-                PATH_STAT(4);
-                k = gload_u16_l2(row + (idx - ns));
+            uint32_t idx, k;
+            bool small;
+            if (SCH == 1) {
+                // the max-ILP build (lone waves): one branch for both rare cases. The bins are searched with the
+                // first word's index, and a lane whose Lemire test may reject redoes the pick inside the branch,
+                // after its rejection loop (C2 8.1 -> 7.5 ms; the occupancy build keeps two branches: C3 +0.8 %)
+                idx = (uint32_t)(m >> 32);
+                small = idx < ns;
+                k = bin_find(small ? idx : 0u);
+                if (nplus_ev & (((uint32_t)m < np) | !small)) {  // Lemire rejection or the large-k row (rare)
+                    if ((uint32_t)m < np) {
+                        PATH_STAT(3);
+                        const uint32_t thr = (0u - np) % np;
+                        while ((uint32_t)m < thr) m = (uint64_t)ws.next() * np;
+                        idx = (uint32_t)(m >> 32);
+                        small = idx < ns;
+                        if (small) k = bin_find(idx);
+                    }
+                    if (!small) {
+                        PATH_STAT(4);
+                        k = gload_u16_l2(row + (idx - ns));
+                    }
+                }
+            } else {
+                if (nplus_ev && (uint32_t)m < np) {
+                    PATH_STAT(3);
+                    const uint32_t thr = (0u - np) % np;
+                    while ((uint32_t)m < thr) m = (uint64_t)ws.next() * np;
+                }
+                idx = (uint32_t)(m >> 32);
+                small = idx < ns;
+                k = bin_find(small ? idx : 0u);
+                if (nplus_ev && !small) {  // large-k row (rare)
+                    PATH_STAT(4);
+                    k = gload_u16_l2(row + (idx - ns));
+                }
             }
 
             CYC_MARK(10);

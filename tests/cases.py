@@ -128,6 +128,11 @@ def bin_cases():
                                               n_replicates=32, max_cells=300, init={36: 3, 2: 5}, bin_kmax=32,
                                               big_cap=200, hist_bins=300, snapshots=[10, 40, 120],
                                               flags=H | B | abi.FLAG_SNAPSHOT_ROWS)
+    # Lemire rejections: with a million N+ cells a pick's low product word falls below n+ with probability
+    # ~2.3e-4 and is rejected with ~2.25e-4 (2^32 mod 1e6 = 967,296), about 30 rejections over the run
+    c["bins_lemire_reject"] = abi.RunSpec(seed=61, process=abi.BIRTH_DEATH, rates=((1.0, 1.0, 0.9, 0.9),),
+                                          n_replicates=64, max_cells=1_100_000, max_iter=4000, cell_cap=1_100_000,
+                                          init={1: 600_000, 3: 400_000}, bin_kmax=32, flags=H | B)
     c["bins_c32"] = abi.RunSpec(seed=46, process=abi.BIRTH_DEATH, rates=BD_RATES, n_replicates=32, max_cells=1500,
                                 cell_cap=70_000, init={1: 2, 70: 1}, flags=H | B)
     c["bins256_c32"] = abi.RunSpec(seed=47, process=abi.BIRTH_DEATH, rates=((1.0, 1.0, 0.9, 0.9),), n_replicates=16,
