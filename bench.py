@@ -417,6 +417,7 @@ def main():
             threads = int(os.environ.get("ECDNA_BENCH_CPU_THREADS", "0")) or usable_cores()
             cpu = cpu_baseline(threads, args.workload)
         chunk, lanes = ctx.geometry()
+        instance = ctx.instance()  # the kernel instance timed (auto rules of ecdna_ssa_ctx_create, ABI v7)
         line = {
             "metric": METRIC if weak else f"Gillespie reaction-events/sec, {args.workload.upper()}",
             "value": events_per_step * args.steps / elapsed,
@@ -445,6 +446,7 @@ def main():
                 "parallelism": f"replicas{n_gpus} ({'contiguous' if weak else 'interleaved'} replicate-id shards, "
                                f"1 RCCL all-reduce of the histogram)",
                 "grid_lanes": lanes,
+                "instance": instance,
                 "kernel_ms_avg": avg_kernel_s * 1e3,
                 "hist_kernel_ms_avg": sum(hist_ms) / len(hist_ms),
                 "kernel_events_per_s_per_gpu": kernel_eps,
@@ -467,6 +469,8 @@ def main():
                     f"sources; counter fields omitted" if pmc.get("stale") else
                     f"profiles/pmc_c3{'_bins' if args.store == 'bins' else ''}.json, round {pmc.get('round')}, "
                     f"git {pmc.get('git_head')}, kernel sources match this build"),
+                # the committed counters describe this instance only if the PMC run chose the same one
+                "pmc_instance_matches": (pmc.get("instance") == instance) if pmc and not pmc.get("stale") else None,
                 "hbm_requests": transactions,
                 "valu_issue": issue,
             },

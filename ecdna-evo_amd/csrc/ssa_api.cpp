@@ -158,6 +158,10 @@ struct Chunk {
     // replicate rotation (bin store; 0 = off): partition size and the counters it starts from
     uint32_t rot_n_pad = 0;
     std::vector<ecdna::RotPart> rot_init;
+    // persistent grid of the chunk and its drain control (admit_slot 0xffffffff: off)
+    uint32_t blocks = 1;
+    uint32_t admit_slot = 0xffffffffu;
+    uint32_t admit_remaining = 0;
 };
 
 }  // namespace
@@ -183,6 +187,7 @@ struct ecdna_ssa_ctx {
     bool refdraws = false;
     uint32_t* d_ref_key = nullptr;
     double* d_ref_btpe = nullptr;
+    uint64_t* d_rng_words = nullptr;  // [n] ChaCha8 stream position of each replicate at its end
     // owned copies of the host inputs
     std::vector<ecdna_rates_t> rates;
     std::vector<uint16_t> init_copies;
@@ -266,6 +271,7 @@ void free_ctx(ecdna_ssa_ctx* c) {
     (void)hipFree(c->d_rot_park);
     (void)hipFree(c->d_ref_key);
     (void)hipFree(c->d_ref_btpe);
+    (void)hipFree(c->d_rng_words);
     (void)hipFree(c->d_hist_own);
     (void)hipFree(c->d_tot_own);
     delete c;
@@ -505,6 +511,7 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
         for (uint64_t k = 10; k < 32768; ++k) btpe_setup(2 * k, bt.data() + k * kBtpeRow);
         CTX_TRY(hipMalloc(&c->d_ref_btpe, bt.size() * sizeof(double)));
         CTX_TRY(hipMemcpy(c->d_ref_btpe, bt.data(), bt.size() * sizeof(double), hipMemcpyHostToDevice));
+        CTX_TRY(hipMalloc(&c->d_rng_words, std::max<uint64_t>(n, 1) * sizeof(uint64_t)));
         c->stepper_block = (uint32_t)ecdna::refdraws_block();
         CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &per_cu, ecdna::refdraws_kernel(p->process, p->segregation), (int)c->stepper_block, 0));
@@ -619,6 +626,24 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
         c->rot_park_min = (int32_t)env_u64("ECDNA_SSA_ROT_PARK_MIN",
                                            std::max<uint64_t>(1, lanes_all * 3 / 2 / ecdna::kRotParts));
     }
+    // grid and drain control per chunk. Drain control (bin store, 256-lane blocks, one wave per SIMD per block):
+    // when lanes run more than two replicates each, the youngest wave slot of every SIMD stops taking fresh
+    // replicates once fewer than 1.5 grids' worth are left (C3: 105 -> 101 ms). ECDNA_SSA_ADMIT=0:
+    // off. Rotation replaces it.
+    for (auto& ch : c->chunks) {
+        const uint32_t per_block = c->bin_ilp == 3 ? c->stepper_block / 2 : c->stepper_block;  // (paired: owners)
+        const uint32_t need = (ch.n + per_block - 1) / per_block;
+        ch.blocks = std::max<uint32_t>(1, std::min<uint32_t>(need, c->stepper_blocks_cap));
+        const uint64_t lanes = (uint64_t)ch.blocks * c->stepper_block;
+        const uint32_t per_cu = c->cus ? (uint32_t)((ch.blocks + c->cus - 1) / c->cus) : 0u;
+        if (!ch.rot_n_pad && c->bin_k && c->stepper_block == 256 && per_cu >= 2 && ch.n > 2 * lanes &&
+            env_u64("ECDNA_SSA_ADMIT", 1)) {
+            const uint32_t slots = (uint32_t)std::min<uint64_t>(env_u64("ECDNA_SSA_ADMIT_SLOTS", 1), per_cu - 1);
+            ch.admit_slot = per_cu - std::max<uint32_t>(slots, 1u);
+            const uint64_t x8 = env_u64("ECDNA_SSA_ADMIT_X8", 12);  // eighths of a grid (tuning)
+            ch.admit_remaining = (uint32_t)std::min<uint64_t>(lanes * x8 / 8, ch.n);
+        }
+    }
     *out = c;
     return ECDNA_OK;
 #undef CTX_TRY
@@ -681,25 +706,10 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
         a.snap_stride = c->out_stride;
         a.big_cap = c->big_cap;
         a.bags = c->d_bags;
-        const uint32_t per_block = c->bin_ilp == 3 ? c->stepper_block / 2 : c->stepper_block;  // (paired: owners)
-        const uint32_t need = (ch.n + per_block - 1) / per_block;
-        const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(need, c->stepper_blocks_cap));
-        // Drain control (bin store, 256-lane blocks, one wave per SIMD per block): when lanes run more than
-        // two replicates each, the youngest wave slot of every SIMD stops taking fresh replicates once
-        // fewer than 1.5 grids' worth are left (C3: 105 -> 101 ms). ECDNA_SSA_ADMIT=0: off.
-        a.admit_slot = 0xffffffffu;
-        a.admit_remaining = 0;
-        const uint64_t lanes = (uint64_t)blocks * c->stepper_block;
-        const uint32_t per_cu = c->cus ? (uint32_t)((blocks + c->cus - 1) / c->cus) : 0u;
-        if (c->bin_k && c->stepper_block == 256 && per_cu >= 2 && ch.n > 2 * lanes &&
-            env_u64("ECDNA_SSA_ADMIT", 1)) {
-            const uint32_t slots = (uint32_t)std::min<uint64_t>(env_u64("ECDNA_SSA_ADMIT_SLOTS", 1), per_cu - 1);
-            a.admit_slot = per_cu - std::max<uint32_t>(slots, 1u);
-            const uint64_t x8 = env_u64("ECDNA_SSA_ADMIT_X8", 12);  // eighths of a grid (tuning)
-            a.admit_remaining = (uint32_t)std::min<uint64_t>(lanes * x8 / 8, ch.n);
-        }
+        const uint32_t blocks = ch.blocks;
+        a.admit_slot = ch.admit_slot;  // (drain control, decided at create)
+        a.admit_remaining = ch.admit_remaining;
         if (ch.rot_n_pad) {  // rotation replaces the drain control
-            a.admit_slot = 0xffffffffu;
             a.rot_parts = c->d_rot_parts;
             a.rot_flags = c->d_rot_flags;
             a.rot_park = c->d_rot_park;
@@ -716,6 +726,7 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
 
         a.ref_key = c->d_ref_key;
         a.ref_btpe = c->d_ref_btpe;
+        a.rng_words = c->d_rng_words ? c->d_rng_words + ch.first : nullptr;
         HIP_TRY(hipEventRecord(ch.ev[0], st));
         if (c->refdraws)
             HIP_TRY(ecdna::launch_refdraws(a, p.process, p.segregation, blocks, st));
@@ -792,6 +803,52 @@ int ecdna_ssa_ctx_geometry(const ecdna_ssa_ctx* c, uint64_t* chunk_replicates, u
     if (!c) return fail(ECDNA_E_INVALID, "ctx is NULL");
     if (chunk_replicates) *chunk_replicates = c->chunk_reps;
     if (grid_lanes) *grid_lanes = (uint64_t)c->stepper_blocks_cap * c->stepper_block;
+    return ECDNA_OK;
+}
+
+int ecdna_ssa_ctx_instance(const ecdna_ssa_ctx* c, ecdna_ssa_instance_t* out) {
+    if (!c || !out) return fail(ECDNA_E_INVALID, "ctx / out is NULL");
+    const ecdna_ssa_params_t& p = c->p;
+    ecdna_ssa_instance_t r{};
+    const void* fn;
+    if (c->refdraws) {
+        r.kernel = ECDNA_KERNEL_REFDRAWS;
+        r.schedule = -1;
+        fn = ecdna::refdraws_kernel(p.process, p.segregation);
+    } else if (c->bin_k) {
+        r.kernel = ECDNA_KERNEL_BINS;
+        r.schedule = c->bin_ilp;
+        r.paired = c->bin_ilp == 3 ? 1 : 0;
+        r.bin_kmax = c->bin_k;
+        r.bin_c32 = (uint32_t)c->bin_c32;
+        r.runtime_flags = (p.flags & (ECDNA_FLAG_TIME_F32 | ECDNA_FLAG_EVENT_HASH)) ? 1 : 0;
+        fn = ecdna::bin_stepper_kernel(p.process, p.segregation, c->bin_k, c->bin_c32, p.flags, c->bin_ilp);
+    } else {
+        r.kernel = ECDNA_KERNEL_ROWS;
+        r.schedule = -1;
+        r.window = (uint32_t)c->window;
+        r.runtime_flags = 1;
+        fn = ecdna::stepper_kernel(p.process, p.segregation, c->window);
+    }
+    for (const auto& ch : c->chunks) {
+        r.rotation += ch.rot_n_pad ? 1 : 0;
+        r.drain_control += ch.admit_slot != 0xffffffffu ? 1 : 0;
+    }
+    r.rot_tick_log2 = (int32_t)c->rot_tick_log2;
+    r.cost_order = c->d_order ? 1 : 0;
+    r.block_lanes = c->stepper_block;
+    r.cus = (uint32_t)c->cus;
+    r.blocks_per_cu = c->cus ? c->stepper_blocks_cap / (uint32_t)c->cus : 0u;
+    r.n_chunks = (uint32_t)c->chunks.size();
+    r.chunk_replicates = c->chunk_reps;
+    r.grid_lanes = (uint64_t)c->stepper_blocks_cap * c->stepper_block;
+    hipFuncAttributes fa{};
+    if (fn && hipFuncGetAttributes(&fa, fn) == hipSuccess) {
+        r.vgprs = (uint32_t)fa.numRegs;
+        r.lds_bytes = (uint32_t)fa.sharedSizeBytes;
+        r.scratch_bytes = (uint32_t)fa.localSizeBytes;
+    }
+    *out = r;
     return ECDNA_OK;
 }
 
@@ -875,6 +932,17 @@ int ecdna_ssa_ctx_download_stats(ecdna_ssa_ctx* c, ecdna_rep_stats_t* out) {
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->last_stream));
     HIP_TRY(hipMemcpy(out, c->d_stats, c->p.n_replicates * sizeof(ecdna_rep_stats_t), hipMemcpyDeviceToHost));
+    return ECDNA_OK;
+}
+
+int ecdna_ssa_ctx_download_rng_words(ecdna_ssa_ctx* c, uint64_t* out) {
+    if (!c) return fail(ECDNA_E_INVALID, "ctx is NULL");
+    if (!c->launched) return fail(ECDNA_E_STATE, "download before launch");
+    if (!c->d_rng_words) return fail(ECDNA_E_STATE, "stream positions need ECDNA_FLAG_REFERENCE_DRAWS");
+    if (!out || !c->p.n_replicates) return ECDNA_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->last_stream));
+    HIP_TRY(hipMemcpy(out, c->d_rng_words, c->p.n_replicates * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return ECDNA_OK;
 }
 

@@ -443,11 +443,19 @@ constexpr int kCpolSc1 = 16;  // buffer cache policy: sc1 (gfx940+ bit 4)
 #ifndef ECDNA_FF_STAY8
 #define ECDNA_FF_STAY8 7   // keep going while >= this many eighths of the entered lanes do
 #endif
+// the entry test is a mask of the wave-uniform iteration counter (ff_tick & (N - 1)): N must be a power of two
+static_assert(ECDNA_FF_TEST_EVERY > 0 && (ECDNA_FF_TEST_EVERY & (ECDNA_FF_TEST_EVERY - 1)) == 0,
+              "ECDNA_FF_TEST_EVERY must be a power of two");
 constexpr uint32_t kFfMax = ECDNA_FF_MAX;  // N- fast-forward: events per full iteration at most
 #ifdef ECDNA_ILP_BUILD
 #define ECDNA_DEV_STATIC static
 #else
 #define ECDNA_DEV_STATIC
+#endif
+
+#ifdef ECDNA_PAIR_CHECK
+// Debug builds (-DECDNA_PAIR_CHECK): paired steps whose helper was out of step with its owner (must stay 0)
+ECDNA_DEV_STATIC __device__ unsigned int g_pair_check;
 #endif
 
 // Development counters of the rotation (built with -DECDNA_ROT_STATS only; tools/rot_stats.py)
@@ -1077,6 +1085,16 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     const uint32_t z2 = __builtin_amdgcn_permlane32_swap(wb.z, wb.z, false, false)[1];
                     const uint32_t w2 = __builtin_amdgcn_permlane32_swap(wb.w, wb.w, false, false)[1];
                     const double lg2 = __longlong_as_double((long long)(((uint64_t)hi2 << 32) | lo2));
+#ifdef ECDNA_PAIR_CHECK
+                    // (debug builds) the helper is still in step: its counter is the owner's e + 1. A helper that
+                    // left early (EXEC at the loop top narrowed by a compiler change) would hand over stale words;
+                    // counted in g_pair_check, and e + 1 is then not committed here (the full event draws it).
+                    const uint32_t hctr = __builtin_amdgcn_permlane32_swap(ctr, ctr, false, false)[1];
+                    const bool pair_ok = helper || hctr == e + 1u;
+                    if (!pair_ok && go) __hip_atomic_fetch_add(&g_pair_check, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+                    constexpr bool pair_ok = true;
+#endif
                     const uint4 wa = wb;
                     const double lga = lg;
                     // the next step's words (events e + 2, e + 3), off this step's chain
@@ -1110,7 +1128,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     const double targetB = fma3((double)y2, 0x1p-32, 0x1p-33) * a0B;
                     const uint32_t chB = (uint32_t)(targetB >= cAB) + (uint32_t)(targetB >= cBB) +
                                          (uint32_t)(targetB >= cCB);
-                    const uint32_t okB = okA & (uint32_t)(e + 1u < a.max_iter) & (uint32_t)(nmB + npf < stop32) &
+                    const uint32_t okB = okA & (uint32_t)pair_ok & (uint32_t)(e + 1u < a.max_iter) & (uint32_t)(nmB + npf < stop32) &
                                          (overB ^ 1u) & (uint32_t)(a0B > 0.0) & (~chB & 1u);
                     const uint32_t nmC = nmB + (uint32_t)(chB == 0u) - (uint32_t)(chB == 2u);
                     const double tauB = div_in_range(lg2, a0B);

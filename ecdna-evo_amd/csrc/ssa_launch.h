@@ -76,6 +76,7 @@ struct StepperArgs {
     // (8 words) and the BTPE constants of Binomial(2k, 1/2) per copy number k (refdraws::kBtpeRow doubles)
     const uint32_t* ref_key;
     const double* ref_btpe;
+    uint64_t* rng_words;            // [n] chunk-offset: ChaCha8 words each replicate's stream handed out (or nullptr)
 };
 
 // Histogram / totals pass over one chunk.

@@ -83,6 +83,9 @@ __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_re
         s->event_hash = hash_on ? h : 0ull;
         s->stop_reason = stop;
         s->error = err;
+        // where the stream stands (words handed out: blocks generated minus those still buffered), for the
+        // reference's subsampling with the same rng after the run (src/main.rs:110-123)
+        if (a.rng_words) a.rng_words[li] = rng.counter * 16ull - (uint64_t)(rng.tail - rng.head);
         active = false;
     };
 

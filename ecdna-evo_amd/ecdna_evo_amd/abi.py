@@ -14,7 +14,7 @@ from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 # ecdna_process_t (ProcessType, src/clap_app.rs:311-315)
 PURE_BIRTH = 0
@@ -99,6 +99,42 @@ FLAG_BIN_STORE = 0x20  # cells binned by copy number; bin_kmax
 # the reference's own draw structure (ChaCha8 streams seed*10+r, first reaction, rand_distr samplers, f32 time;
 # row store only): seed for seed the oracle's compat mode
 FLAG_REFERENCE_DRAWS = 0x40
+
+
+# ecdna_ssa_instance_t (ABI v7): the kernel instance a context launches (ecdna_ssa_ctx_instance)
+KERNEL_KINDS = {0: "ssa_stepper (rows)", 1: "ssa_stepper_bins (bins)", 2: "ssa_stepper_refdraws (reference draws)"}
+SCHEDULE_NAMES = {-1: "n/a", 0: "occupancy-first", 1: "max-ILP", 2: "occupancy-first, 128-VGPR cap", 3: "max-ILP, paired lanes"}
+
+
+class Instance(C.Structure):
+    _fields_ = [
+        ("kernel", C.c_int32),
+        ("schedule", C.c_int32),
+        ("paired", C.c_int32),
+        ("rotation", C.c_int32),
+        ("rot_tick_log2", C.c_int32),
+        ("drain_control", C.c_int32),
+        ("cost_order", C.c_int32),
+        ("runtime_flags", C.c_int32),
+        ("bin_kmax", C.c_uint32),
+        ("bin_c32", C.c_uint32),
+        ("block_lanes", C.c_uint32),
+        ("blocks_per_cu", C.c_uint32),
+        ("cus", C.c_uint32),
+        ("n_chunks", C.c_uint32),
+        ("vgprs", C.c_uint32),
+        ("lds_bytes", C.c_uint32),
+        ("scratch_bytes", C.c_uint32),
+        ("window", C.c_uint32),
+        ("chunk_replicates", C.c_uint64),
+        ("grid_lanes", C.c_uint64),
+    ]
+
+    def as_dict(self) -> dict:
+        d = {f: int(getattr(self, f)) for f, _ in self._fields_}
+        d["kernel_name"] = KERNEL_KINDS.get(d["kernel"], "?")
+        d["schedule_name"] = SCHEDULE_NAMES.get(d["schedule"], "?")
+        return d
 
 
 SNAPSHOT_DTYPE = np.dtype([("time", "<f8"), ("nminus", "<u8"), ("nplus", "<u8"), ("taken", "<u4"),

@@ -35,8 +35,10 @@ EXPORTS = [
     "ecdna_ssa_ctx_download",
     "ecdna_ssa_ctx_download_snapshots",
     "ecdna_ssa_ctx_download_stats",
+    "ecdna_ssa_ctx_download_rng_words",
     "ecdna_ssa_ctx_row_stride",
     "ecdna_ssa_ctx_geometry",
+    "ecdna_ssa_ctx_instance",
     "ecdna_ssa_ctx_destroy",
     "ecdna_ssa_comm_unique_id",
     "ecdna_ssa_comm_init_rank",
@@ -97,10 +99,14 @@ def lib():
     L.ecdna_ssa_ctx_download_snapshots.restype = C.c_int
     L.ecdna_ssa_ctx_download_stats.argtypes = [C.c_void_p, C.c_void_p]
     L.ecdna_ssa_ctx_download_stats.restype = C.c_int
+    L.ecdna_ssa_ctx_download_rng_words.argtypes = [C.c_void_p, C.c_void_p]
+    L.ecdna_ssa_ctx_download_rng_words.restype = C.c_int
     L.ecdna_ssa_ctx_row_stride.argtypes = [C.c_void_p]
     L.ecdna_ssa_ctx_row_stride.restype = C.c_int64
     L.ecdna_ssa_ctx_geometry.argtypes = [C.c_void_p, P(C.c_uint64), P(C.c_uint64)]
     L.ecdna_ssa_ctx_geometry.restype = C.c_int
+    L.ecdna_ssa_ctx_instance.argtypes = [C.c_void_p, P(abi.Instance)]
+    L.ecdna_ssa_ctx_instance.restype = C.c_int
     L.ecdna_ssa_ctx_destroy.argtypes = [C.c_void_p]
     L.ecdna_ssa_ctx_destroy.restype = C.c_int
     L.ecdna_ssa_comm_unique_id.argtypes = [C.c_void_p]
@@ -175,6 +181,7 @@ class Result:
         self.snapshots = None  # [n][S] abi.SNAPSHOT_DTYPE
         self.snapshot_rows = None  # [n][S][stride] u16 under FLAG_SNAPSHOT_ROWS
         self.stats = None  # [n] abi.STATS_DTYPE under FLAG_REP_STATS
+        self.rng_words = None  # [n] u64 under FLAG_REFERENCE_DRAWS: ChaCha8 stream position at the end
 
     def row(self, i: int) -> np.ndarray:
         return self.rows[i, : int(self.summaries[i]["nplus"])]
@@ -227,6 +234,12 @@ class Context:
         _check(lib().ecdna_ssa_ctx_geometry(self.h, C.byref(a), C.byref(b)), "geometry")
         return a.value, b.value
 
+    def instance(self) -> dict:
+        """The kernel instance this context launches (schedule, pairing, rotation, K, VGPRs, ...): ABI v7."""
+        ins = abi.Instance()
+        _check(lib().ecdna_ssa_ctx_instance(self.h, C.byref(ins)), "instance")
+        return ins.as_dict()
+
     def row_stride(self) -> int:
         return int(lib().ecdna_ssa_ctx_row_stride(self.h))
 
@@ -261,6 +274,10 @@ class Context:
             st = np.zeros(p.n_replicates, dtype=abi.STATS_DTYPE)
             _check(lib().ecdna_ssa_ctx_download_stats(self.h, st.ctypes.data), "download_stats")
             res.stats = st
+        if p.flags & abi.FLAG_REFERENCE_DRAWS:
+            w = np.zeros(p.n_replicates, dtype=np.uint64)
+            _check(lib().ecdna_ssa_ctx_download_rng_words(self.h, w.ctypes.data), "download_rng_words")
+            res.rng_words = w
         return res
 
 

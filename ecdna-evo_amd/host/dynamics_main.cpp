@@ -63,6 +63,7 @@ struct Options {
     bool dry_run = false;
     bool rows = false;       // --cell-store rows
     uint32_t bin_kmax = 64;  // --bin-kmax
+    bool has_cell_store = false, has_bin_kmax = false;
     bool reference_draws = false;  // --draws reference
     std::string pooled;            // --pooled FILE
 };
@@ -224,10 +225,12 @@ Options parse(int argc, char** argv) {
             const std::string v = need(a);
             if (v != "bins" && v != "rows") usage_error("--cell-store must be bins or rows");
             o.rows = v == "rows";
+            o.has_cell_store = true;
         } else if (a == "--bin-kmax") {
             const uint64_t v = parse_u64(a, need(a));
             if (v != 64 && v != 256) usage_error("--bin-kmax must be 64 or 256");
             o.bin_kmax = (uint32_t)v;
+            o.has_bin_kmax = true;
         } else if (a == "--draws") {
             const std::string v = need(a);
             if (v != "philox" && v != "reference") usage_error("--draws must be philox or reference");
@@ -249,7 +252,10 @@ Options parse(int argc, char** argv) {
         usage_error("the argument '--years <YEARS>' cannot be used with '--cells <CELLS>'");
     if (o.debug && (o.has_years || o.has_cells || o.sequential || o.has_runs || o.verbosity))
         usage_error("the argument '--debug' cannot be used with the other run options");
-    if (o.reference_draws) o.rows = true;  // the reference's draws address cells in swap_remove order
+    // the reference's draws address cells in swap_remove order: the row store, never the bins
+    if (o.reference_draws && ((o.has_cell_store && !o.rows) || o.has_bin_kmax))
+        usage_error("the argument '--draws reference' cannot be used with '--cell-store bins' or '--bin-kmax'");
+    if (o.reference_draws) o.rows = true;
     return o;
 }
 
@@ -328,21 +334,6 @@ void shard_of(uint64_t runs, int gpus, int g, uint64_t& first, uint64_t& n) {
     n = runs * (uint64_t)(g + 1) / (uint64_t)gpus - first;
 }
 
-// Every shard thread reaches the reduction (an RCCL collective: all ranks must join) or none does.
-struct Rendezvous {
-    std::mutex mu;
-    std::condition_variable cv;
-    int arrived = 0, failed = 0, total = 0;
-    bool all_ok(bool ok) {
-        std::unique_lock<std::mutex> lk(mu);
-        arrived += 1;
-        failed += ok ? 0 : 1;
-        if (arrived == total) cv.notify_all();
-        cv.wait(lk, [&] { return arrived == total; });
-        return failed == 0;
-    }
-};
-
 struct Shard {
     int device;
     uint64_t first, n;
@@ -353,12 +344,13 @@ struct Shard {
     std::vector<uint16_t> rows;
     std::vector<ecdna_snapshot_t> snap_meta;
     std::vector<uint16_t> snap_rows;
+    std::vector<uint64_t> rng_words;  // --draws reference: each replicate's ChaCha8 position at its end
     int64_t stride = 0;
     int rc = 0;
     std::string err;
 };
 
-void run_shard(const ecdna_ssa_params_t& base, Shard& sh, Rendezvous* rv) {
+void run_shard(const ecdna_ssa_params_t& base, Shard& sh, ecdna::host::Rendezvous* rv) {
     ecdna_ssa_params_t p = base;
     p.device = sh.device;
     p.first_replicate = sh.first;
@@ -384,16 +376,23 @@ void run_shard(const ecdna_ssa_params_t& base, Shard& sh, Rendezvous* rv) {
         sh.snap_rows.resize(sh.n * p.n_snapshots * st);
         sh.rc = ecdna_ssa_ctx_download_snapshots(c, sh.snap_meta.data(), sh.snap_rows.data());
     }
+    if (!sh.rc && (p.flags & ECDNA_FLAG_REFERENCE_DRAWS)) {  // where each replicate's rng stands (subsampling)
+        sh.rng_words.resize(sh.n);
+        sh.rc = ecdna_ssa_ctx_download_rng_words(c, sh.rng_words.data());
+    }
     if (rv) {  // --pooled: the run's histogram and totals, all-reduced over the devices' shards (RCCL)
-        const bool ok = rv->all_ok(sh.rc == 0);
-        if (ok) {
-            sh.rc = ecdna_ssa_ctx_reduce(c, sh.comm);
+        const int rc = ecdna::host::join_reduction(*rv, sh.rc, [&] {
+            int q = ecdna_ssa_ctx_reduce(c, sh.comm);
             sh.hist.resize((uint64_t)p.n_param_sets * p.hist_bins);
             sh.totals.resize(p.n_param_sets);
-            if (!sh.rc) sh.rc = ecdna_ssa_ctx_download(c, nullptr, sh.hist.data(), sh.totals.data(), nullptr);
-        } else if (!sh.rc) {
+            if (!q) q = ecdna_ssa_ctx_download(c, nullptr, sh.hist.data(), sh.totals.data(), nullptr);
+            return q;
+        });
+        if (!sh.rc && rc == ecdna::host::kPeerFailed) {
             sh.rc = ECDNA_E_STATE;
             sh.err = "another device's shard failed; no reduction";
+        } else if (!sh.rc) {
+            sh.rc = rc;
         }
     }
     if (sh.rc && sh.err.empty()) sh.err = ecdna_ssa_last_error_message();
@@ -480,7 +479,7 @@ int main(int argc, char** argv) {
         shards[g].device = g;
         shard_of(r.runs, gpus, g, shards[g].first, shards[g].n);
     }
-    Rendezvous rv;
+    ecdna::host::Rendezvous rv;
     rv.total = gpus;
     std::vector<void*> comms;
     if (!o.pooled.empty() && r.runs) {  // one RCCL communicator per device (ncclCommInitAll)
@@ -493,7 +492,7 @@ int main(int argc, char** argv) {
         }
         for (int g = 0; g < gpus; ++g) shards[g].comm = comms[g];
     }
-    Rendezvous* rvp = comms.empty() ? nullptr : &rv;
+    ecdna::host::Rendezvous* rvp = comms.empty() ? nullptr : &rv;
     std::vector<std::thread> th;
     for (int g = 1; g < gpus; ++g)
         if (shards[g].n) th.emplace_back(run_shard, std::cref(p), std::ref(shards[g]), rvp);
@@ -540,8 +539,15 @@ int main(int argc, char** argv) {
                 const uint16_t* row = sh.rows.data() + i * (uint64_t)sh.stride;
                 fin.nplus.assign(row, row + s.nplus);
                 ecdna::host::save(o.path, filename, (float)s.time, fin);
-                for (size_t k = 0; k < o.subsamples.size(); ++k) {  // src/main.rs:110-123
-                    Distribution sub = ecdna::host::subsample(fin, o.subsamples[k], o.seed, rep, (uint32_t)k);
+                // subsamples (src/main.rs:110-123, 184-197): under --draws reference with the replicate's own ChaCha8
+                // stream, continued where the run left it and chained from one subsample to the next, as the
+                // reference's `into_subsampled(*nb_cells, &mut rng)` loop does; else from a Philox region of the
+                // replicate's key that the stepper never touches
+                uint64_t word_pos = o.reference_draws ? sh.rng_words[i] : 0;
+                for (size_t k = 0; k < o.subsamples.size(); ++k) {
+                    Distribution sub = o.reference_draws
+                                           ? ecdna::host::subsample_reference(fin, o.subsamples[k], o.seed, idx, word_pos)
+                                           : ecdna::host::subsample(fin, o.subsamples[k], o.seed, rep, (uint32_t)k);
                     ecdna::host::save(o.path, filename, (float)s.time, sub);
                 }
                 if (r.verbosity > 0)  // src/main.rs:205-210
@@ -553,7 +559,11 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "error: %s\n", e.what());
         return 1;
     }
-    if (!o.pooled.empty() && !shards.empty() && !shards[0].hist.empty()) {  // every shard holds the reduced sums
+    if (!o.pooled.empty()) {  // every shard holds the reduced sums
+        if (shards[0].hist.empty()) {  // --runs 0: nothing ran, an empty pool (there is always one shard)
+            shards[0].hist.assign(p.hist_bins, 0);
+            shards[0].totals.assign(1, ecdna_totals_t{});
+        }
         const ecdna_totals_t& t = shards[0].totals[0];
         std::string js = "{\"histogram\":{";
         bool first = true;

@@ -11,6 +11,7 @@
 #include <fstream>
 #include <set>
 #include <sstream>
+#include <unordered_set>
 
 namespace ecdna {
 namespace host {
@@ -267,6 +268,137 @@ Distribution subsample(const Distribution& d, uint64_t nb_cells, uint64_t seed, 
         else
             out.nplus.push_back(d.nplus[idx - d.nminus]);
     }
+    return out;
+}
+
+namespace {
+
+// rand_chacha 0.3.1 ChaCha8Rng: ChaCha with 8 rounds, 64-bit block counter in words 12-13, stream in words
+// 14-15, handed out one 32-bit word at a time in block order (rand_core BlockRng over a 4-block buffer; the
+// buffer only batches blocks, so the word sequence is the blocks' words in counter order). Key:
+// seed_from_u64 = rand_core 0.6.4's PCG32 expansion of the u64 seed into 8 little-endian words.
+struct ChaCha8Stream {
+    uint32_t in[16];
+    uint32_t blk[16];
+    uint64_t pos;       // words handed out
+    uint64_t blk_id = ~0ull;
+
+    ChaCha8Stream(uint64_t seed, uint64_t stream, uint64_t word_pos) : pos(word_pos) {
+        in[0] = 0x61707865u;
+        in[1] = 0x3320646eu;
+        in[2] = 0x79622d32u;
+        in[3] = 0x6b206574u;
+        uint64_t st = seed;
+        for (int i = 0; i < 8; ++i) {
+            st = st * 6364136223846793005ull + 11634580027462260723ull;
+            const uint32_t xs = (uint32_t)(((st >> 18) ^ st) >> 27), rot = (uint32_t)(st >> 59);
+            in[4 + i] = (xs >> rot) | (xs << ((32u - rot) & 31u));
+        }
+        in[14] = (uint32_t)stream;
+        in[15] = (uint32_t)(stream >> 32);
+    }
+    static uint32_t rotl(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+    void block(uint64_t b) {
+        in[12] = (uint32_t)b;
+        in[13] = (uint32_t)(b >> 32);
+        uint32_t x[16];
+        std::memcpy(x, in, sizeof(x));
+        auto qr = [&](int a, int bb, int c, int d) {
+            x[a] += x[bb]; x[d] ^= x[a]; x[d] = rotl(x[d], 16);
+            x[c] += x[d]; x[bb] ^= x[c]; x[bb] = rotl(x[bb], 12);
+            x[a] += x[bb]; x[d] ^= x[a]; x[d] = rotl(x[d], 8);
+            x[c] += x[d]; x[bb] ^= x[c]; x[bb] = rotl(x[bb], 7);
+        };
+        for (int r = 0; r < 8; r += 2) {
+            qr(0, 4, 8, 12); qr(1, 5, 9, 13); qr(2, 6, 10, 14); qr(3, 7, 11, 15);
+            qr(0, 5, 10, 15); qr(1, 6, 11, 12); qr(2, 7, 8, 13); qr(3, 4, 9, 14);
+        }
+        for (int i = 0; i < 16; ++i) blk[i] = x[i] + in[i];
+        blk_id = b;
+    }
+    uint32_t next_u32() {
+        const uint64_t b = pos >> 4;
+        if (b != blk_id) block(b);
+        return blk[pos++ & 15u];
+    }
+    // rand 0.8.5 UniformInt<u32>::sample_single_inclusive(low, high): next_u32 widened by range, conservative
+    // zone (range << lz(range)) - 1
+    uint32_t range_incl(uint32_t low, uint32_t high) {
+        const uint32_t range = high - low + 1u;
+        if (range == 0) return next_u32();
+        const uint32_t zone = (range << __builtin_clz(range)) - 1u;
+        for (;;) {
+            const uint64_t m = (uint64_t)next_u32() * range;
+            if ((uint32_t)m <= zone) return low + (uint32_t)(m >> 32);
+        }
+    }
+    // rand 0.8.5 Uniform::new(0, n) over u32, sampled: the exact zone u32::MAX - (2^32 - n) % n
+    uint32_t uniform(uint32_t n) {
+        const uint32_t zone = 0xffffffffu - (uint32_t)((0x100000000ull - n) % n);
+        for (;;) {
+            const uint64_t m = (uint64_t)next_u32() * n;
+            if ((uint32_t)m <= zone) return (uint32_t)(m >> 32);
+        }
+    }
+};
+
+// rand 0.8.5 seq::index::sample(rng, length, amount), length < 2^32: its algorithm choice (f32 arithmetic) and
+// each algorithm's draws; the chosen indices (their order does not matter to a histogram, the draws do).
+std::vector<uint32_t> index_sample(ChaCha8Stream& rng, uint32_t length, uint32_t amount) {
+    const int j = length < 500000u ? 0 : 1;
+    int alg;  // 0 Floyd, 1 in place, 2 rejection
+    if (amount < 163u) {
+        const float c0[2] = {1.6f, 8.0f / 45.0f}, c1[2] = {10.0f, 70.0f / 9.0f};
+        const float a = (float)amount;
+        alg = (amount > 11u && (float)length < (c1[j] + c0[j] * a) * a) ? 1 : 0;
+    } else {
+        const float c[2] = {270.0f, 330.0f / 9.0f};
+        alg = ((float)length < c[j] * (float)amount) ? 1 : 2;
+    }
+    std::vector<uint32_t> idx;
+    idx.reserve(amount);
+    if (alg == 0) {
+        const bool shuffle_after = amount >= 50u;  // below 50: Floyd's fully shuffled variant (inserts, no draws)
+        std::unordered_set<uint32_t> taken;
+        for (uint32_t jj = length - amount; jj < length; ++jj) {
+            const uint32_t t = rng.range_incl(0u, jj);
+            idx.push_back(taken.insert(t).second ? t : jj);
+            if (idx.back() == jj) taken.insert(jj);
+        }
+        if (shuffle_after)
+            for (uint32_t i = amount - 1; i >= 1; --i) std::swap(idx[i], idx[rng.range_incl(0u, i)]);
+    } else if (alg == 1) {
+        std::vector<uint32_t> all(length);
+        for (uint32_t i = 0; i < length; ++i) all[i] = i;
+        for (uint32_t i = 0; i < amount; ++i) std::swap(all[i], all[rng.range_incl(i, length - 1u)]);
+        idx.assign(all.begin(), all.begin() + amount);
+    } else {
+        std::unordered_set<uint32_t> cache;
+        for (uint32_t q = 0; q < amount; ++q) {
+            uint32_t pos = rng.uniform(length);
+            while (!cache.insert(pos).second) pos = rng.uniform(length);
+            idx.push_back(pos);
+        }
+    }
+    return idx;
+}
+
+}  // namespace
+
+Distribution subsample_reference(const Distribution& d, uint64_t nb_cells, uint64_t seed, uint64_t stream,
+                                 uint64_t& word_pos) {
+    const uint64_t N = d.cells();
+    if (N > 0xffffffffull) throw IoError("subsampling needs fewer than 2^32 cells");
+    const uint32_t amount = (uint32_t)std::min<uint64_t>(nb_cells, N);  // choose_multiple clamps the amount
+    ChaCha8Stream rng(seed, stream, word_pos);
+    Distribution out;
+    for (uint32_t i : index_sample(rng, (uint32_t)N, amount)) {
+        if (i < d.nminus)
+            out.nminus += 1;
+        else
+            out.nplus.push_back(d.nplus[i - d.nminus]);
+    }
+    word_pos = rng.pos;
     return out;
 }
 

@@ -7,8 +7,10 @@
 // C ABI (include/ecdna_ssa.h).
 #pragma once
 
+#include <condition_variable>
 #include <cstdint>
 #include <map>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -55,6 +57,46 @@ std::vector<uint64_t> default_snapshots(uint64_t cells, uint32_t n_snapshots = 1
 // the replicate's Philox stream in a region the stepper never uses: key (seed lo, seed hi), counter
 // (sample index, 0x80000000 | block, rid lo, rid hi). nb_cells >= cells returns the whole distribution.
 Distribution subsample(const Distribution& d, uint64_t nb_cells, uint64_t seed, uint64_t rid, uint32_t sample_index);
+
+// into_subsampled under the reference's own draws (--draws reference): the reference subsamples with the SAME
+// rng that ran the replicate (`into_subsampled(*nb_cells, &mut rng)`, src/main.rs:110-123, 184-197), so this
+// continues ChaCha8Rng::seed_from_u64(seed) on stream `stream` (= seed * 10 + idx) at word `word_pos` (where the
+// stepper left it, ecdna_ssa_ctx_download_rng_words) and advances word_pos past the words it uses. ecdna-lib
+// 3.0.2's into_subsampled is not vendored; reconstructed (parity unpinned): the cells in the order
+// [n- N- cells, then the N+ cells in Vec order], min(nb_cells, cells) of them chosen by rand 0.8.5
+// SliceRandom::choose_multiple, i.e. seq::index::sample (Floyd / in-place / rejection by its size rule).
+Distribution subsample_reference(const Distribution& d, uint64_t nb_cells, uint64_t seed, uint64_t stream,
+                                 uint64_t& word_pos);
+
+// The multi-device --pooled reduction (ecdna-dynamics --gpus N): one host thread per device shard, and the
+// histogram all-reduce is an RCCL collective that every rank must join. Every shard thread reaches the
+// rendezvous; the collective runs only if all shards succeeded, else no thread calls it (a rank that skips a
+// collective its peers entered would hang them).
+struct Rendezvous {
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0, failed = 0, total = 0;
+    bool all_ok(bool ok) {
+        std::unique_lock<std::mutex> lk(mu);
+        arrived += 1;
+        failed += ok ? 0 : 1;
+        if (arrived == total) cv.notify_all();
+        cv.wait(lk, [&] { return arrived == total; });
+        return failed == 0;
+    }
+};
+
+constexpr int kPeerFailed = -1000;  // join_reduction: another shard failed, the collective was skipped
+
+// A shard's part of the reduction: rc = its own status so far; reduce() runs the collective (and download) and
+// returns its status. Returns reduce()'s status when every shard succeeded, kPeerFailed when this shard
+// succeeded but another did not, and rc (unchanged) when this shard itself failed.
+template <class Reduce>
+int join_reduction(Rendezvous& rv, int rc, Reduce&& reduce) {
+    const bool all = rv.all_ok(rc == 0);
+    if (rc) return rc;
+    return all ? reduce() : kPeerFailed;
+}
 
 }  // namespace host
 }  // namespace ecdna

@@ -46,6 +46,24 @@ int ecdna_host_subsample(const uint16_t* nplus, uint64_t n_plus, uint64_t nminus
     }
 }
 
+// into_subsampled under the reference's draws (the replicate's ChaCha8 stream continued at *word_pos).
+int ecdna_host_subsample_reference(const uint16_t* nplus, uint64_t n_plus, uint64_t nminus, uint64_t nb_cells,
+                                   uint64_t seed, uint64_t stream, uint64_t* word_pos, uint16_t* out_nplus,
+                                   uint64_t* out_n_plus, uint64_t* out_nminus) {
+    try {
+        ecdna::host::Distribution d;
+        d.nminus = nminus;
+        if (n_plus) d.nplus.assign(nplus, nplus + n_plus);
+        ecdna::host::Distribution s = ecdna::host::subsample_reference(d, nb_cells, seed, stream, *word_pos);
+        if (!s.nplus.empty()) std::memcpy(out_nplus, s.nplus.data(), s.nplus.size() * sizeof(uint16_t));
+        *out_n_plus = s.nplus.size();
+        *out_nminus = s.nminus;
+        return 0;
+    } catch (...) {
+        return -1;
+    }
+}
+
 // save() into dir; writes the created path.
 int ecdna_host_save(const char* dir, const char* filename, float time, const uint16_t* nplus, uint64_t n_plus,
                     uint64_t nminus, char* out_path, size_t n) {

@@ -10,6 +10,8 @@
  *   ecdna_host_save           process::save of one distribution                   src/process.rs:31-55
  *   ecdna_host_load           EcDNADistribution::load for --initial               src/clap_app.rs:177-192
  *   ecdna_host_subsample      EcDNADistribution::into_subsampled (no replacement) src/main.rs:110-123
+ *   ecdna_host_subsample_reference  the same, continuing the replicate's ChaCha8 rng src/main.rs:110-123,
+ *                                                                                 184-197
  *
  * String outputs: written NUL-terminated to out[0..n); the return value is the string length, or -1
  * when the buffer is too small or the call failed. */
@@ -45,6 +47,16 @@ int64_t ecdna_host_load(const char* path, uint16_t* out_nplus, uint64_t cap, uin
 int ecdna_host_subsample(const uint16_t* nplus, uint64_t n_plus, uint64_t nminus, uint64_t nb_cells, uint64_t seed,
                          uint64_t rid, uint32_t sample_index, uint16_t* out_nplus, uint64_t* out_n_plus,
                          uint64_t* out_nminus);
+/* into_subsampled under the reference's own draws: the reference subsamples with the rng that ran the
+ * replicate (src/main.rs:110-123, 184-197), so this continues ChaCha8Rng::seed_from_u64(seed), stream `stream`
+ * (= seed*10 + idx), at word *word_pos (ecdna_ssa_ctx_download_rng_words; advanced past the words used, so
+ * consecutive subsamples of one replicate chain as in the reference's loop). Reconstruction of ecdna-lib 3.0.2
+ * (not vendored; parity unpinned): cells ordered [n- N- cells, then the N+ cells in order], min(nb_cells,
+ * cells) chosen by rand 0.8.5 SliceRandom::choose_multiple (seq::index::sample). out_nplus needs
+ * min(nb_cells, n_plus) entries. Returns 0, or -1 on failure. */
+int ecdna_host_subsample_reference(const uint16_t* nplus, uint64_t n_plus, uint64_t nminus, uint64_t nb_cells,
+                                   uint64_t seed, uint64_t stream, uint64_t* word_pos, uint16_t* out_nplus,
+                                   uint64_t* out_n_plus, uint64_t* out_nminus);
 
 #ifdef __cplusplus
 }

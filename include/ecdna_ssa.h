@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ECDNA_SSA_ABI_VERSION 6
+#define ECDNA_SSA_ABI_VERSION 7
 
 /* Process type — ProcessType (src/clap_app.rs:311-315); chosen as BirthDeath
  * when d0 > 0 or d1 > 0 (src/clap_app.rs:163-174, 194-200). */
@@ -282,10 +282,49 @@ int ecdna_ssa_ctx_download(ecdna_ssa_ctx* c, ecdna_rep_summary_t* out_summaries,
 int ecdna_ssa_ctx_download_snapshots(ecdna_ssa_ctx* c, ecdna_snapshot_t* meta, uint16_t* rows);
 /* Per-replicate statistics of the last launch (needs ECDNA_FLAG_REP_STATS): out[n_replicates]. */
 int ecdna_ssa_ctx_download_stats(ecdna_ssa_ctx* c, ecdna_rep_stats_t* out);
+/* Reference draws (ECDNA_FLAG_REFERENCE_DRAWS, ABI v7): per replicate, the number of 32-bit words its ChaCha8
+ * stream (seed_from_u64(seed), stream seed*10 + r) had handed out when it stopped — where the reference's
+ * end-of-run subsampling continues the same rng (into_subsampled(nb, &mut rng), src/main.rs:110-123, 184-197;
+ * ecdna_host_subsample_reference). out[n_replicates]. */
+int ecdna_ssa_ctx_download_rng_words(ecdna_ssa_ctx* c, uint64_t* out);
 /* Row stride (cells) of the rows buffer, or 0 when the run is chunked (rows not downloadable). */
 int64_t ecdna_ssa_ctx_row_stride(const ecdna_ssa_ctx* c);
 /* Replicates per chunk (memory bound) and lanes of the persistent stepper grid. */
 int ecdna_ssa_ctx_geometry(const ecdna_ssa_ctx* c, uint64_t* chunk_replicates, uint64_t* grid_lanes);
+
+/* The kernel instance a context launches (ABI v7): every choice ecdna_ssa_ctx_create makes from the
+ * workload shape and the ECDNA_SSA_* environment knobs, so that a benchmark line can name
+ * the instance it timed and a flip of an automatic rule shows up in its output. Results never depend on
+ * any of these; they are speed choices. */
+typedef enum {
+    ECDNA_KERNEL_ROWS = 0,       /* ssa_stepper: the row store (one u16 per cell in HBM) */
+    ECDNA_KERNEL_BINS = 1,       /* ssa_stepper_bins: the bin store (ECDNA_FLAG_BIN_STORE) */
+    ECDNA_KERNEL_REFDRAWS = 2    /* ssa_stepper_refdraws: the reference draws (ECDNA_FLAG_REFERENCE_DRAWS) */
+} ecdna_kernel_kind_t;
+typedef struct {
+    int32_t kernel;            /* ecdna_kernel_kind_t */
+    int32_t schedule;          /* bin stepper: 0 occupancy-first, 1 max-ILP, 2 occupancy-first capped at 128
+                                  VGPRs (K = 64 / u16), 3 max-ILP with paired lanes; -1 for the other kernels */
+    int32_t paired;            /* 1: lane l < 32 owns a replicate, lane l + 32 helps its N- fast-forward */
+    int32_t rotation;          /* number of chunks whose replicates rotate through the lanes */
+    int32_t rot_tick_log2;     /* rotation tick (loop iterations, log2) */
+    int32_t drain_control;     /* number of chunks whose youngest wave slots stop admitting replicates early */
+    int32_t cost_order;        /* 1: replicates start costliest set first (params.set_cost_hint) */
+    int32_t runtime_flags;     /* 1: the instance reads f32 time / event hash from the flags (TF = 1) */
+    uint32_t bin_kmax;         /* bin store: binned copy numbers (0 for the other kernels) */
+    uint32_t bin_c32;          /* bin store: 1 = u32 counters, 0 = u16 */
+    uint32_t block_lanes;      /* workgroup size */
+    uint32_t blocks_per_cu;    /* resident workgroups per CU of the persistent grid */
+    uint32_t cus;              /* compute units of the device */
+    uint32_t n_chunks;         /* launches per run (HBM-bounded chunks) */
+    uint32_t vgprs;            /* per lane, as compiled (hipFuncGetAttributes numRegs) */
+    uint32_t lds_bytes;        /* static LDS per workgroup */
+    uint32_t scratch_bytes;    /* private segment per lane */
+    uint32_t window;           /* row store: 1 = LDS tail window variant */
+    uint64_t chunk_replicates; /* replicates per chunk */
+    uint64_t grid_lanes;       /* lanes of the persistent grid */
+} ecdna_ssa_instance_t;
+int ecdna_ssa_ctx_instance(const ecdna_ssa_ctx* c, ecdna_ssa_instance_t* out);
 int ecdna_ssa_ctx_destroy(ecdna_ssa_ctx* c);
 
 /* ---- Multi-GPU reduction (ABI v6; RCCL over xGMI).

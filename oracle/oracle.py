@@ -57,6 +57,11 @@ def lib():
     L.oracle_decrease_nplus.restype = C.c_int
     L.oracle_set_snapshot_outputs.argtypes = [C.c_void_p, C.c_void_p]
     L.oracle_set_snapshot_outputs.restype = None
+    L.oracle_set_rng_words_output.argtypes = [C.c_void_p]
+    L.oracle_set_rng_words_output.restype = None
+    L.oracle_compat_subsample.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
+                                          P(C.c_uint64), C.c_void_p]
+    L.oracle_compat_subsample.restype = C.c_int64
     L.oracle_increase_nminus.argtypes = [C.c_void_p]
     L.oracle_increase_nminus.restype = C.c_int
     L.oracle_decrease_nminus.argtypes = [C.c_void_p]
@@ -134,16 +139,34 @@ def run(spec: "abi.RunSpec", mode: str = "philox", n_threads: int = 0, want_rows
     srows = np.zeros((n, S, p.cell_cap), dtype=np.uint16) if (S and p.flags & abi.FLAG_SNAPSHOT_ROWS) else None
     lib().oracle_set_snapshot_outputs(meta.ctypes.data if meta is not None else None,
                                       srows.ctypes.data if srows is not None else None)
+    words = np.zeros(n, dtype=np.uint64) if mode == "compat" else None
+    lib().oracle_set_rng_words_output(words.ctypes.data if words is not None else None)
     try:
         rc = fn(C.byref(p), summ.ctypes.data, hist.ctypes.data, tot.ctypes.data,
                 rows.ctypes.data if rows is not None else None, stride, n_threads)
     finally:
         lib().oracle_set_snapshot_outputs(None, None)
+        lib().oracle_set_rng_words_output(None)
     if rc != 0:
         raise ValueError(f"oracle run failed: {rc}")
     res = OracleResult(summ, hist.reshape(p.n_param_sets, p.hist_bins), tot, rows, stride)
     res.snapshots, res.snapshot_rows = meta, srows
+    res.rng_words = words  # compat: ChaCha8 words each replicate's stream handed out
     return res
+
+
+def compat_subsample(nplus_cells, nminus: int, nb_cells: int, seed: int, stream: int, word_pos: int):
+    """ecdna-lib into_subsampled as reconstructed (oracle_compat_subsample): the chosen cells' copy numbers
+    (0 = N-) in index-vector order, and the stream's word position after it."""
+    cells = np.ascontiguousarray(np.asarray(nplus_cells, dtype=np.uint16))
+    total = len(cells) + int(nminus)
+    out = np.zeros(max(1, min(int(nb_cells), total)), dtype=np.uint16)
+    wp = C.c_uint64(int(word_pos))
+    k = lib().oracle_compat_subsample(cells.ctypes.data if len(cells) else None, len(cells), int(nminus),
+                                      int(nb_cells), int(seed), int(stream), C.byref(wp), out.ctypes.data)
+    if k < 0:
+        raise ValueError("oracle_compat_subsample failed")
+    return out[:k], wp.value
 
 
 class Distr(C.Structure):

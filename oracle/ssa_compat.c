@@ -81,7 +81,10 @@ struct oracle_chacha {
     uint32_t st[16];
     uint32_t buf[64];
     uint32_t idx;
+    uint64_t words; /* words handed out so far (the stream position) */
 };
+
+static void chacha_refill(oracle_chacha* r);
 
 static void chacha_init(oracle_chacha* r, uint64_t seed, uint64_t stream) {
     r->st[0] = 0x61707865u;
@@ -94,6 +97,21 @@ static void chacha_init(oracle_chacha* r, uint64_t seed, uint64_t stream) {
     r->st[14] = (uint32_t)stream;
     r->st[15] = (uint32_t)(stream >> 32);
     r->idx = 64;
+    r->words = 0;
+}
+
+/* The stream continued at word position `pos` (rand_chacha's set_word_pos): the 4-block buffer that holds
+ * word pos starts at block 4 * (pos / 64); the next word is its pos % 64. */
+static void chacha_seek(oracle_chacha* r, uint64_t pos) {
+    const uint64_t blk = (pos / 64u) * 4u;
+    r->st[12] = (uint32_t)blk;
+    r->st[13] = (uint32_t)(blk >> 32);
+    r->idx = 64;
+    r->words = pos;
+    if (pos % 64u) {
+        chacha_refill(r);
+        r->idx = (uint32_t)(pos % 64u);
+    }
 }
 
 static void chacha_refill(oracle_chacha* r) {
@@ -106,6 +124,7 @@ static void chacha_refill(oracle_chacha* r) {
 }
 
 static inline uint32_t cc_u32(oracle_chacha* r) {
+    r->words += 1;
     if (r->idx >= 64) {
         chacha_refill(r);
         r->idx = 0;
@@ -115,6 +134,7 @@ static inline uint32_t cc_u32(oracle_chacha* r) {
 
 /* rand_core BlockRng::next_u64: two consecutive words, low first, spanning a refill. */
 static inline uint64_t cc_u64(oracle_chacha* r) {
+    r->words += 2;
     if (r->idx < 63) {
         uint64_t lo = r->buf[r->idx], hi = r->buf[r->idx + 1];
         r->idx += 2;
@@ -172,7 +192,7 @@ static inline double float_1_2(uint64_t bits) {
  * wedge, BTPE). glibc rounds those to within 0.52 ulp, not always correctly, and a GPU has no glibc, so the
  * compat mapping defines log and exp as the CORRECTLY ROUNDED functions, computed in double-double
  * (~2^-97 relative) from basic IEEE operations and explicit fma in a fixed order; the GPU compat stepper
- * (ecdna-evo_amd/csrc/compat_math.hpp) restates the same operations, so both agree bit for bit, and both
+ * (ecdna-evo_amd/csrc/refdraws.hpp: log_cr, exp_cr, exp_approx) restates the same operations, so both agree bit for bit, and both
  * agree with glibc wherever glibc rounds correctly (tests/test_compat_math.py). */
 #include "compat_tables.h"
 
@@ -476,7 +496,7 @@ void oracle_snapshot_check(const ecdna_ssa_params_t* p, uint32_t* sj, uint64_t n
 
 void oracle_compat_simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16_t* row,
                                       ecdna_rep_summary_t* out, ecdna_snapshot_t* snap_meta, uint16_t* snap_rows,
-                                      uint64_t snap_stride) {
+                                      uint64_t snap_stride, uint64_t* out_words) {
     uint32_t sj = 0;
     const uint64_t set = rid / p->reps_per_set;
     const ecdna_rates_t rt = p->rates[set];
@@ -621,4 +641,133 @@ void oracle_compat_simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid,
     out->event_hash = hash_on ? h : 0;
     out->stop_reason = stop;
     out->error = err;
+    if (out_words) *out_words = rng.words;
+}
+
+/* ------------------------------------------------ end-of-run subsampling */
+
+/* rand 0.8.5 gen_range over u32 (UniformInt<u32>::sample_single_inclusive(low, high)): widening multiply of
+ * next_u32 by range = high - low + 1 with the conservative zone (range << lz(range)) - 1. */
+static uint32_t gen_range_u32_incl(oracle_chacha* r, uint32_t low, uint32_t high) {
+    const uint32_t range = high - low + 1u;
+    if (range == 0) return cc_u32(r); /* the whole u32 range */
+    const uint32_t zone = (range << __builtin_clz(range)) - 1u;
+    for (;;) {
+        const uint64_t m = (uint64_t)cc_u32(r) * range;
+        if ((uint32_t)m <= zone) return low + (uint32_t)(m >> 32);
+    }
+}
+
+/* rand 0.8.5 Uniform::new(0, length) over u32 (UniformInt::new_inclusive + sample): the exact zone
+ * u32::MAX - (2^32 - range) % range. */
+static uint32_t uniform_u32(oracle_chacha* r, uint32_t length) {
+    const uint32_t range = length;
+    const uint32_t z = (uint32_t)((0x100000000ull - range) % range);
+    const uint32_t zone = 0xffffffffu - z;
+    for (;;) {
+        const uint64_t m = (uint64_t)cc_u32(r) * range;
+        if ((uint32_t)m <= zone) return (uint32_t)(m >> 32);
+    }
+}
+
+static int idx_cmp(const void* a, const void* b) {
+    const uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
+    return x < y ? -1 : x > y;
+}
+
+/* rand 0.8.5 seq::index::sample(rng, length, amount) for length <= u32::MAX: the algorithm by its size rule
+ * (f32 arithmetic, as published), the index vector in the algorithm's order. out[amount]. */
+static void index_sample(oracle_chacha* r, uint32_t length, uint32_t amount, uint32_t* out) {
+    int alg; /* 0 floyd, 1 inplace, 2 rejection */
+    const int j = length < 500000u ? 0 : 1;
+    if (amount < 163u) {
+        const float c0[2] = {1.6f, 8.0f / 45.0f}, c1[2] = {10.0f, 70.0f / 9.0f};
+        const float amount_fp = (float)amount;
+        const float m4 = c0[j] * amount_fp;
+        alg = (amount > 11u && (float)length < (c1[j] + m4) * amount_fp) ? 1 : 0;
+    } else {
+        const float c[2] = {270.0f, 330.0f / 9.0f};
+        alg = ((float)length < c[j] * (float)amount) ? 1 : 2;
+    }
+    if (alg == 0) { /* sample_floyd */
+        const int floyd_shuffle = amount < 50u;
+        uint32_t len = 0;
+        for (uint32_t jj = length - amount; jj < length; ++jj) {
+            const uint32_t t = gen_range_u32_incl(r, 0u, jj);
+            int64_t pos = -1;
+            for (uint32_t q = 0; q < len; ++q)
+                if (out[q] == t) {
+                    pos = q;
+                    break;
+                }
+            if (pos >= 0) {
+                if (floyd_shuffle) { /* indices.insert(pos, j) */
+                    memmove(out + pos + 1, out + pos, (len - (uint32_t)pos) * sizeof(uint32_t));
+                    out[pos] = jj;
+                } else {
+                    out[len] = jj;
+                }
+                ++len;
+                continue;
+            }
+            out[len++] = t;
+        }
+        if (!floyd_shuffle)
+            for (uint32_t i = amount - 1; i >= 1; --i) { /* SliceRandom::shuffle with u32 indices */
+                const uint32_t k = gen_range_u32_incl(r, 0u, i);
+                const uint32_t tmp = out[i];
+                out[i] = out[k];
+                out[k] = tmp;
+            }
+    } else if (alg == 1) { /* sample_inplace */
+        uint32_t* idx = malloc((size_t)length * sizeof(uint32_t));
+        for (uint32_t i = 0; i < length; ++i) idx[i] = i;
+        for (uint32_t i = 0; i < amount; ++i) {
+            const uint32_t k = gen_range_u32_incl(r, i, length - 1u); /* gen_range(i..length) */
+            const uint32_t tmp = idx[i];
+            idx[i] = idx[k];
+            idx[k] = tmp;
+        }
+        memcpy(out, idx, (size_t)amount * sizeof(uint32_t));
+        free(idx);
+    } else { /* sample_rejection: draws until amount distinct indices (a set of those seen) */
+        uint32_t* seen = malloc((size_t)amount * sizeof(uint32_t)); /* sorted */
+        uint32_t ns = 0;
+        for (uint32_t q = 0; q < amount; ++q) {
+            for (;;) {
+                const uint32_t pos = uniform_u32(r, length);
+                uint32_t lo = 0, hi = ns;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) / 2;
+                    if (seen[mid] < pos) lo = mid + 1;
+                    else hi = mid;
+                }
+                if (lo < ns && seen[lo] == pos) continue; /* cache.insert(pos) failed */
+                memmove(seen + lo + 1, seen + lo, (ns - lo) * sizeof(uint32_t));
+                seen[lo] = pos;
+                ++ns;
+                out[q] = pos;
+                break;
+            }
+        }
+        free(seen);
+    }
+    (void)idx_cmp;
+}
+
+int64_t oracle_compat_subsample(const uint16_t* nplus_cells, uint64_t nplus, uint64_t nminus, uint64_t nb_cells,
+                                uint64_t seed, uint64_t stream, uint64_t* word_pos, uint16_t* out_cells) {
+    const uint64_t cells = nplus + nminus;
+    if (cells > 0xffffffffull) return -1;
+    const uint32_t amount = (uint32_t)(nb_cells < cells ? nb_cells : cells); /* choose_multiple clamps */
+    oracle_chacha rng;
+    chacha_init(&rng, seed, stream);
+    chacha_seek(&rng, *word_pos);
+    uint32_t* idx = malloc(((size_t)amount + 1) * sizeof(uint32_t));
+    index_sample(&rng, (uint32_t)cells, amount, idx);
+    for (uint32_t q = 0; q < amount; ++q)
+        out_cells[q] = idx[q] < nminus ? (uint16_t)0 : nplus_cells[idx[q] - nminus];
+    free(idx);
+    *word_pos = rng.words;
+    return amount;
 }

@@ -417,6 +417,7 @@ typedef struct {
     int compat;
     ecdna_snapshot_t* snap_meta;
     uint16_t* snap_rows;
+    uint64_t* rng_words; /* compat: [n] ChaCha8 words handed out per replicate, or NULL */
 } run_ctx;
 
 #define FNV_OFFSET 0xcbf29ce484222325ull
@@ -431,6 +432,10 @@ void oracle_set_snapshot_outputs(ecdna_snapshot_t* meta, uint16_t* rows) {
     tl_snap_meta = meta;
     tl_snap_rows = rows;
 }
+
+static _Thread_local uint64_t* tl_rng_words = NULL;
+
+void oracle_set_rng_words_output(uint64_t* words) { tl_rng_words = words; }
 
 /* The snapshot rule at the top of advance_step (src/process.rs:122-145, 267-290): while the deque is
  * non-empty and ANY remaining snapshot equals n- + n+, pop the FRONT snapshot and save the current
@@ -627,7 +632,7 @@ static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16
 /* from ssa_compat.c */
 void oracle_compat_simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16_t* row,
                                       ecdna_rep_summary_t* out, ecdna_snapshot_t* snap_meta, uint16_t* snap_rows,
-                                      uint64_t snap_stride);
+                                      uint64_t snap_stride, uint64_t* out_words);
 
 static void accumulate(const ecdna_ssa_params_t* p, uint64_t rid, const uint16_t* row,
                        const ecdna_rep_summary_t* s, uint64_t* hist, ecdna_totals_t* tot) {
@@ -668,7 +673,8 @@ static void* worker(void* arg) {
         ecdna_snapshot_t* sm = c->snap_meta ? c->snap_meta + i * S : NULL;
         uint16_t* sr = c->snap_rows ? c->snap_rows + i * S * p->cell_cap : NULL;
         if (c->compat)
-            oracle_compat_simulate_replicate(p, rid, row, &s, sm, sr, p->cell_cap);
+            oracle_compat_simulate_replicate(p, rid, row, &s, sm, sr, p->cell_cap,
+                                             c->rng_words ? c->rng_words + i : NULL);
         else
             simulate_replicate(p, rid, row, &s, sm, sr, p->cell_cap);
         if (c->summaries) c->summaries[i] = s;
@@ -765,6 +771,7 @@ static int run_pool(const ecdna_ssa_params_t* p, ecdna_rep_summary_t* out_summar
     c.compat = compat;
     c.snap_meta = tl_snap_meta;
     c.snap_rows = tl_snap_rows;
+    c.rng_words = compat ? tl_rng_words : NULL;
     if (c.snap_meta) memset(c.snap_meta, 0, p->n_replicates * p->n_snapshots * sizeof(ecdna_snapshot_t));
     if (n_threads <= 0) n_threads = (int)sysconf(_SC_NPROCESSORS_ONLN);
     if (n_threads < 1) n_threads = 1;

@@ -44,6 +44,10 @@ int oracle_run_philox(const ecdna_ssa_params_t* p, ecdna_rep_summary_t* out_summ
 /* Snapshot outputs for the next oracle_run_* call on this thread (NULL = discard):
  * meta[n_replicates][n_snapshots], rows[n_replicates][n_snapshots][row_stride]. */
 void oracle_set_snapshot_outputs(ecdna_snapshot_t* meta, uint16_t* rows);
+/* Compat mode: per replicate, the number of 32-bit words its ChaCha8 stream handed out by the end of the
+ * run (the position where the reference's subsampling continues the same rng, src/main.rs:110-123) for the
+ * next oracle_run_compat call on this thread (NULL = discard): words[n_replicates]. */
+void oracle_set_rng_words_output(uint64_t* words);
 /* Reference-semantics CPU path: stream of global replicate r is seed*10 + r (src/main.rs:56-58,
  * 213-215). Time is always accumulated in f32 like process.time (src/process.rs:184, 336);
  * ECDNA_FLAG_EVENT_HASH is honoured, ECDNA_FLAG_TIME_F32 is implied. */
@@ -91,6 +95,15 @@ uint64_t oracle_chacha_next_u64(oracle_chacha* r);
 uint64_t oracle_compat_gen_range(oracle_chacha* r, uint64_t n);   /* rand 0.8.5 gen_range(0..n) */
 double oracle_compat_exp1(oracle_chacha* r);                        /* rand_distr Exp1 (ziggurat) */
 uint64_t oracle_compat_binomial(oracle_chacha* r, uint64_t n, double p); /* rand_distr Binomial */
+/* ecdna-lib 3.0.2 EcDNADistribution::into_subsampled(nb_cells, rng) as reconstructed (not
+ * vendored, parity unpinned): the cells in the order [n- N- cells (copy number 0), then the N+ cells in
+ * Vec order], min(nb_cells, cells) of them drawn without replacement (CHANGELOG.md:213-216) by rand 0.8.5
+ * SliceRandom::choose_multiple = seq::index::sample (Floyd / in-place / rejection by its size rule), from the
+ * ChaCha8 stream `stream` of seed_from_u64(seed) continued at word *word_pos (advanced past the words used).
+ * out_cells[min(nb_cells, cells)] receives the chosen cells' copy numbers in index-vector order. Returns
+ * the number chosen, or -1 when there are 2^32 or more cells. */
+int64_t oracle_compat_subsample(const uint16_t* nplus_cells, uint64_t nplus, uint64_t nminus, uint64_t nb_cells,
+                                uint64_t seed, uint64_t stream, uint64_t* word_pos, uint16_t* out_cells);
 /* The compat mapping's ln and exp: correctly rounded (double-double), DESIGN.md §4.1. */
 double oracle_compat_log(double x);
 double oracle_compat_exp(double x);

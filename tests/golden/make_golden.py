@@ -12,8 +12,14 @@ run, so these fixtures are regression pins of the oracle i
                        the engine's ECDNA_FLAG_REFERENCE_DRAWS mode must reproduce bit for bit.
   c3_compat_seed42.npz, c4_subset_compat_seed42.npz, c5_shaped_compat_seed42.npz
                        reference-semantics runs of the birth-death configurations: C3 (65,536 replicates),
-                       16 sets of the C4 sweep x 4,096 replicates, C5's turnover process to 2e4 cells (4,096
+                       16 sets of the C4 sweep x 16,384 replicates (ABC rejects per set, abc.md:38-55, so each
+                       set's law is held to KS < 0.01 on its own), C5's turnover process to 2e4 cells (4,096
                        replicates): pooled histograms + per-replicate final n-, n+, events, stop reason.
+  c3cap_compat_seed42.npz
+                       C3 under the other plausible reading of sosa's cell cap: the
+                       cap tested against the sum of BirthDeath's duplicated population vector [n-, n+, n-, n+]
+                       (src/process.rs:339-344), i.e. a stop at n- + n+ >= max_cells / 2
+                       (ECDNA_FLAG_BD_CAP_COMPAT); 65,536 replicates.
   c2_compat_seed42.npz reference-semantics run (ChaCha8 streams seed*10+i, first-reaction, BTPE) of
                        the C2 shape: 65,536 replicates, pure birth + binomial to 1e4 cells, seed 42:
                        pooled copy-number histogram + per-replicate final n-/n+. The GPU KS test
@@ -106,7 +112,7 @@ def c3_spec(n=C3_REPS, **kw):
 # k0 in {1, 16, 128} (bench.py workload_spec("c4") grid: set i has s = 1 + 1.5 (i % 16) / 15,
 # d = 0.7 ((i // 16) % 8) / 7, k0 = 2^(i // 128))
 C4_SETS = [0, 21, 42, 63, 85, 112, 527, 533, 550, 567, 585, 620, 903, 920, 938, 1023]
-C4_REPS = 4096
+C4_REPS = 16384
 
 
 def c4_subset_spec(reps_per_set=C4_REPS, **kw):
@@ -141,9 +147,12 @@ def _per_replicate(r):
                 iters=s["iters"].astype(np.uint32), stop_reason=s["stop_reason"].astype(np.uint8))
 
 
-def make_bd_compat():
+def make_bd_compat(only=None):
     for name, spec in (("c3_compat_seed42", c3_spec()), ("c4_subset_compat_seed42", c4_subset_spec()),
-                       ("c5_shaped_compat_seed42", c5_shaped_spec())):
+                       ("c5_shaped_compat_seed42", c5_shaped_spec()),
+                       ("c3cap_compat_seed42", c3_spec(flags=abi.FLAG_BD_CAP_COMPAT))):
+        if only and not name.startswith(only + "_"):
+            continue
         r = oracle.run(spec, mode="compat")
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **_per_replicate(r))
 
@@ -159,6 +168,7 @@ def make_c2():
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", choices=["parity", "c2", "refdraws", "bd"])
+    ap.add_argument("--bd", choices=["c3", "c4_subset", "c5_shaped", "c3cap"], help="with --only bd: one fixture")
     a = ap.parse_args()
     oracle.build()
     if a.only in (None, "parity"):
@@ -168,4 +178,4 @@ if __name__ == "__main__":
     if a.only in (None, "refdraws"):
         make_refdraws()
     if a.only in (None, "bd"):
-        make_bd_compat()
+        make_bd_compat(a.bd)

@@ -73,6 +73,9 @@ def test_struct_layout_matches_header(tmp_path):
         lines.append(f'printf(", \\"s_{f}\\": %zu", offsetof(ecdna_rep_summary_t, {f}));')
     for f in abi.TOTALS_DTYPE.names:
         lines.append(f'printf(", \\"t_{f}\\": %zu", offsetof(ecdna_totals_t, {f}));')
+    lines.append('printf(", \\"instance\\": %zu", sizeof(ecdna_ssa_instance_t));')
+    for f, _ in abi.Instance._fields_:
+        lines.append(f'printf(", \\"i_{f}\\": %zu", offsetof(ecdna_ssa_instance_t, {f}));')
     lines += ['printf("}\\n");', "return 0;}"]
     src.write_text("\n".join(lines))
     exe = tmp_path / "layout"
@@ -89,6 +92,9 @@ def test_struct_layout_matches_header(tmp_path):
         assert got[f"s_{f}"] == abi.SUMMARY_DTYPE.fields[f][1], f
     for f in abi.TOTALS_DTYPE.names:
         assert got[f"t_{f}"] == abi.TOTALS_DTYPE.fields[f][1], f
+    assert got["instance"] == C.sizeof(abi.Instance)
+    for f, _ in abi.Instance._fields_:
+        assert got[f"i_{f}"] == getattr(abi.Instance, f).offset, f
 
 
 def _has_gpu(lib):
@@ -203,4 +209,6 @@ def test_reduce_entry_points_validate_arguments(product_lib):
     out = C.c_void_p()
     assert L.ecdna_ssa_comm_init_rank(uid, 2, 5, 0, C.byref(out)) == abi.E_INVALID  # rank >= n_ranks
     assert L.ecdna_ssa_comm_destroy(None) == 0
+    L.ecdna_ssa_ctx_instance.argtypes = [C.c_void_p, C.c_void_p]
+    assert L.ecdna_ssa_ctx_instance(None, None) == abi.E_INVALID
     assert L.ecdna_ssa_strerror(abi.E_COMM)

@@ -2,7 +2,7 @@
 
 The reference calls glibc's log and exp (Rust f64::ln / f64::exp) inside rand_distr's Exp1 ziggurat and BTPE
 binomial. The compat mapping defines them as the CORRECTLY ROUNDED functions, restated on the CPU
-(oracle/ssa_compat.c) and the GPU (ecdna-evo_amd/csrc/compat_math.hpp) with the same operations, so the two
+(oracle/ssa_compat.c) and the GPU (ecdna-evo_amd/csrc/refdraws.hpp: log_cr / exp_cr / exp_approx) with the same operations, so the two
 agree bit for bit. These tests pin:
   * compat_log / compat_exp against exact decimal arithmetic (correct rounding), and
   * against glibc (what the Rust reference calls): equal except where glibc itself misrounds (it guarantees

@@ -38,3 +38,32 @@ def test_oracle_reproduces_c2_compat_fixture(oracle_mod):
     np.testing.assert_array_equal(r.hist[0], g["hist"])
     np.testing.assert_array_equal(r.summaries["nminus"], g["nminus"])
     np.testing.assert_array_equal(r.summaries["nplus"], g["nplus"])
+
+
+@pytest.mark.parametrize("name", ["c3", "c3cap", "c4_subset", "c5_shaped"])
+def test_oracle_reproduces_bd_compat_fixture_heads(oracle_mod, name):
+    """The committed birth-death reference-semantics fixtures are the compat oracle's output: the first
+    replicates of every fixture (of every parameter set for the C4 subset) are recomputed and compared."""
+    import make_golden
+    from ecdna_evo_amd import abi
+
+    g = np.load(os.path.join(GOLDEN, f"{name}_compat_seed42.npz"))
+    if name == "c4_subset":
+        m = make_golden.C4_REPS
+        for i in range(16):
+            spec = make_golden.c4_subset_spec(first_replicate=i * m, n_replicates=16)
+            r = oracle_mod.run(spec, mode="compat", n_threads=8)
+            for f in ("nminus", "nplus", "iters", "stop_reason"):
+                np.testing.assert_array_equal(r.summaries[f].astype(np.int64),
+                                              g[f][i * m:i * m + 16].astype(np.int64), err_msg=f"set {i}: {f}")
+        return
+    mk = {"c3": make_golden.c3_spec, "c5_shaped": make_golden.c5_shaped_spec,
+          "c3cap": lambda **kw: make_golden.c3_spec(flags=abi.FLAG_BD_CAP_COMPAT, **kw)}[name]
+    n = 16 if name == "c5_shaped" else 256
+    r = oracle_mod.run(mk(n=n), mode="compat", n_threads=8)
+    for f in ("nminus", "nplus", "iters", "stop_reason"):
+        np.testing.assert_array_equal(r.summaries[f].astype(np.int64), g[f][:n].astype(np.int64), err_msg=f)
+    if name == "c3cap":
+        s = r.summaries
+        full = s["stop_reason"] == abi.STOP_MAX_CELLS
+        assert full.any() and np.all((s["nminus"] + s["nplus"])[full] == 5_000)

@@ -1,0 +1,113 @@
+"""The exact kernel instances the bench lines time, checked bit for bit at full size.
+
+bench.py picks its instance per workload through ecdna_ssa_ctx_create's automatic rules (schedule, paired lanes,
+rotation, K, the cost-ordered start): the C4 and C5 throughput claims rest on instances that the small parity
+cases only cover in miniature. Each test below builds bench.py's own RunSpec (bench.workload_spec) for a
+workload as the bench runs it — same flags (no event hash: the hash selects a different template instance),
+same K, big_cap and cost hint, same shard layout — asserts the instance the context chose
+(ecdna_ssa_ctx_instance, ABI v7), so the test fails if an automatic rule stops choosing it, then runs the whole
+shard and compares a sample of its replicates with the philox oracle field by field (summaries incl. the f64 time
+bits; the birth-death paths of src/main.rs:130-173)."""
+import dataclasses
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from ecdna_evo_amd import abi, shard
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def _bench():
+    import importlib
+
+    return importlib.import_module("bench")
+
+
+def _run_with_instance(engine_mod, spec):
+    with engine_mod.Context(spec) as ctx:
+        ins = ctx.instance()
+        ctx.launch()
+        ctx.sync()
+        return ins, ctx.download()
+
+
+def _compare_sample(res, spec, oracle_mod, local, n, threads=8):
+    """Local replicates local .. local + n - 1 of `res` against the oracle run of the same global ids."""
+    stride = spec.stride()
+    sub = dataclasses.replace(spec, first_replicate=spec.first_replicate + local * stride, n_replicates=n, _keep=[])
+    c = oracle_mod.run(sub, mode="philox", n_threads=threads)
+    for f in c.summaries.dtype.names:
+        a, b = res.summaries[f][local:local + n], c.summaries[f]
+        if f == "time":
+            a, b = a.view(np.uint64), b.view(np.uint64)
+        np.testing.assert_array_equal(a, b, err_msg=f"replicates {local}..{local + n - 1}: {f}")
+    assert np.all(c.summaries["iters"] > 0)
+
+
+@pytest.mark.gpu
+def test_c5_bench_shard_instance_bit_exact(engine_mod, oracle_mod):
+    """C5 8-GPU rank-0 shard as bench.py runs it (interleaved ids 0, 8, 16, ...; 32,768 replicates; K = 64 with u32
+    counters; large-k row 2^16; f64 time, no hash): paired lanes under the max-ILP schedule; replicates 0..3 (about
+    2e7 events each, to 1e6 cells) equal the oracle."""
+    bench = _bench()
+    first, n, stride = shard.interleaved_range(0, 8, 262_144)
+    spec = bench.workload_spec(first, n, 262_144, workload="c5", stride=stride)
+    assert spec.flags == abi.FLAG_BIN_STORE and spec.bin_kmax == 64 and spec.big_cap == 1 << 16
+    ins, res = _run_with_instance(engine_mod, spec)
+    assert (ins["kernel"], ins["schedule"], ins["paired"], ins["bin_kmax"], ins["bin_c32"]) == (1, 3, 1, 64, 1), ins
+    assert ins["runtime_flags"] == 0 and ins["rotation"] == 0 and ins["n_chunks"] == 1, ins
+    s = res.summaries
+    assert np.all(s["error"] == 0)
+    assert set(s["stop_reason"].tolist()) <= {abi.STOP_MAX_CELLS, abi.STOP_MAX_TIME, abi.STOP_ABSORBING}
+    _compare_sample(res, spec, oracle_mod, 0, 4, threads=4)
+    assert np.all(s["nminus"][:4] + s["nplus"][:4] == 1_000_000)  # these four reach the cap
+
+
+@pytest.mark.gpu
+def test_c4_bench_shard_instance_bit_exact(engine_mod, oracle_mod):
+    """C4 8-GPU rank-3 shard as bench.py runs it (interleaved ids 3, 11, ...; 524,288 replicates over all 1024 sets;
+    K = 64 / u16; costliest sets first from set_cost_hint): the max-ILP schedule without rotation; 64 replicates of
+    set 1000 (k0 = 128: 256-bit binomials, cells beyond the bins) and 64 of set 37 (k0 = 1) equal the oracle."""
+    bench = _bench()
+    first, n, stride = shard.interleaved_range(3, 8, 4_194_304)
+    spec = bench.workload_spec(first, n, 4_194_304, workload="c4", stride=stride)
+    assert spec.set_cost_hint is not None and spec.bin_kmax == 64 and spec.flags == abi.FLAG_BIN_STORE
+    ins, res = _run_with_instance(engine_mod, spec)
+    assert (ins["kernel"], ins["schedule"], ins["paired"], ins["bin_kmax"], ins["bin_c32"]) == (1, 1, 0, 64, 0), ins
+    assert ins["cost_order"] == 1 and ins["rotation"] == 0 and ins["runtime_flags"] == 0, ins
+    assert np.all(res.summaries["error"] == 0) and np.all(res.totals["replicates"] == 512)
+    for set_id in (1000, 37):
+        m0 = (set_id * 4096 - first + stride - 1) // stride  # first local replicate of the set
+        _compare_sample(res, spec, oracle_mod, m0, 64)
+
+
+@pytest.mark.gpu
+def test_c4_bench_whole_instance_bit_exact(engine_mod, oracle_mod):
+    """C4 on one GPU as `bench.py --workload c4` runs it (4,194,304 replicates, K = 64 / u16, cost-ordered starts,
+    16 replicates per lane): the 128-VGPR occupancy build (schedule 2) with the drain control, no rotation (a cost
+    hint is given); samples of sets 1023 (k0 = 128, the costliest), 512 and 0 equal the oracle."""
+    bench = _bench()
+    spec = bench.workload_spec(0, 4_194_304, 4_194_304, workload="c4")
+    ins, res = _run_with_instance(engine_mod, spec)
+    assert (ins["kernel"], ins["schedule"], ins["paired"], ins["bin_kmax"], ins["bin_c32"]) == (1, 2, 0, 64, 0), ins
+    assert ins["cost_order"] == 1 and ins["rotation"] == 0 and ins["drain_control"] == 1, ins
+    assert np.all(res.summaries["error"] == 0) and np.all(res.totals["replicates"] == 4096)
+    for set_id in (1023, 512, 0):
+        _compare_sample(res, spec, oracle_mod, set_id * 4096 + 1000, 48)
+
+
+@pytest.mark.gpu
+def test_c3_bench_instance_bit_exact(engine_mod, oracle_mod):
+    """C3, the metric's line (2^20 replicates, K = 32 / u32, rotation): the occupancy-first schedule with rotation
+    on; replicates spread over the id range equal the oracle."""
+    bench = _bench()
+    spec = bench.workload_spec(0, 1 << 20, 1 << 20, workload="c3")
+    ins, res = _run_with_instance(engine_mod, spec)
+    assert (ins["kernel"], ins["schedule"], ins["paired"], ins["bin_kmax"], ins["bin_c32"]) == (1, 0, 0, 32, 1), ins
+    assert ins["rotation"] == 1 and ins["runtime_flags"] == 0, ins
+    for local in (0, 333_333, (1 << 20) - 256):
+        _compare_sample(res, spec, oracle_mod, local, 256)

@@ -30,7 +30,9 @@ def hist_json(nminus, cells):
     return h
 
 
-def expected_files(spec, res, b, subsamples):
+def expected_files(spec, res, b, subsamples, reference=False):
+    """reference: --draws reference, whose subsamples continue each replicate's ChaCha8 stream where the run left it
+    (res.rng_words), chained over the subsample sizes (src/main.rs:110-123; oracle.compat_subsample)."""
     out = {}
     bd = spec.process == abi.BIRTH_DEATH
     for i in range(spec.n_replicates):
@@ -49,10 +51,21 @@ def expected_files(spec, res, b, subsamples):
         s = res.summaries[i]
         row = res.row(i)
         put(s["nminus"], row, s["time"])
+        word = int(res.rng_words[i]) if reference else 0
         for k, nb in enumerate(subsamples):
-            p, m = subsample_py(row.tolist(), int(s["nminus"]), nb, spec.seed, i, k)
+            if reference:
+                cells, word = oracle_compat_subsample(row, int(s["nminus"]), nb, spec.seed, idx, word)
+                p, m = [int(c) for c in cells if c], int(np.sum(cells == 0))
+            else:
+                p, m = subsample_py(row.tolist(), int(s["nminus"]), nb, spec.seed, i, k)
             put(m, p, s["time"])
     return out
+
+
+def oracle_compat_subsample(*a):
+    import oracle
+
+    return oracle.compat_subsample(*a)
 
 
 def written_files(root):
@@ -78,7 +91,9 @@ CASES = {
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_cli_writes_what_the_reference_writes(name, store, engine_mod, oracle_mod, tmp_path):
     """store "reference": --draws reference, the Rust binary's own draw structure (ChaCha8 + rand_distr), so
-    every snapshot and end-of-run file equals the compat oracle's seed for seed."""
+    every snapshot and end-of-run file equals the compat oracle's seed for seed, and the subsample files continue
+    each replicate's own ChaCha8 stream as the reference's `into_subsampled(n, &mut rng)` does (src/main.rs:110-123;
+    ecdna-lib's into_subsampled reconstructed, parity unpinned: DESIGN.md §10)."""
     args, c = CASES[name]
     extra = ["--draws", "reference"] if store == "reference" else ["--cell-store", store]
     out = subprocess.run([CLI, *args, *extra, str(tmp_path)], capture_output=True, text=True, timeout=300)
@@ -90,7 +105,7 @@ def test_cli_writes_what_the_reference_writes(name, store, engine_mod, oracle_mo
                        snapshots=snaps, bin_kmax=64 if store == "bins" else 0,
                        flags=abi.FLAG_TIME_F32 | abi.FLAG_SNAPSHOT_ROWS | (abi.FLAG_BIN_STORE if store == "bins" else 0))
     res = oracle_mod.run(spec, mode="compat" if store == "reference" else "philox", want_rows=True)
-    want = expected_files(spec, res, c["rates"], c["subs"])
+    want = expected_files(spec, res, c["rates"], c["subs"], reference=store == "reference")
     got = written_files(tmp_path)
     assert set(got) == set(want)
     for k in want:
@@ -119,3 +134,14 @@ def test_cli_pooled_histogram_is_the_reduced_run(store, engine_mod, tmp_path):
     assert (got["replicates"], got["events"], got["nminus"], got["nplus"], got["errors"]) == \
         (64, int(t["events"]), int(t["nminus"]), int(t["nplus"]), 0)
     assert got["stop_reasons"] == [int(x) for x in t["stop_reasons"]]
+
+
+@pytest.mark.gpu
+def test_cli_pooled_with_zero_runs_writes_an_empty_pool(engine_mod, tmp_path):
+    """--pooled with --runs 0 writes an empty pooled histogram (no replicate ran) instead of no file."""
+    pooled = tmp_path / "pooled.json"
+    out = subprocess.run([CLI, "--runs", "0", "--pooled", str(pooled), str(tmp_path / "out")], capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    got = json.load(open(pooled))
+    assert got["histogram"] == {} and got["replicates"] == 0 and got["events"] == 0

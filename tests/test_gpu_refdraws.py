@@ -38,6 +38,9 @@ def test_gpu_reference_draws_match_compat_oracle(name, engine_mod, oracle_mod):
     gpu = engine_mod.run(spec, want_rows=True)
     cpu = oracle_mod.run(spec, mode="compat", want_rows=True)
     _compare(gpu, cpu, name)
+    # where each replicate's ChaCha8 stream stands at its end (the reference's subsampling continues it,
+    # src/main.rs:110-123; ecdna_ssa_ctx_download_rng_words)
+    np.testing.assert_array_equal(gpu.rng_words, cpu.rng_words, err_msg=name)
 
 
 @pytest.mark.gpu
@@ -68,3 +71,4 @@ def test_gpu_reference_draws_c3_sample(engine_mod, oracle_mod):
             a, b = a.view(np.uint64), b.view(np.uint64)
         np.testing.assert_array_equal(a, b, err_msg=f)
     np.testing.assert_array_equal(g.hist, c.hist)
+    np.testing.assert_array_equal(g.rng_words, c.rng_words)

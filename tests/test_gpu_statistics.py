@@ -317,22 +317,50 @@ def test_c3_ks_against_reference_semantics(engine_mod, store):
 @pytest.mark.parametrize("store", sorted(BENCH_STORES))
 def test_c4_subset_ks_against_reference_semantics(engine_mod, store):
     """16 sets of the C4 ABC sweep spanning s in [1, 2.5], d in [0, 0.7] and k0 in {1, 16, 128} (bench settings:
-    bin store K = 64), 16,384 replicates per set against the fixture's 4,096: pooled KS < 0.01 over all sets;
-    per set, KS below the two-sample critical value at alpha = 1e-4 (replicate counts; CPU null max 0.0065)
-    and per-replicate laws."""
+    bin store K = 64), 65,536 replicates per set against the fixture's 16,384. ABC rejection is per parameter set
+    (abc.md:38-55), so EACH set is held to the north star's KS < 0.01 on its own pooled copy-number histogram (the
+    old 4,096-replicate fixture only allowed the alpha = 1e-4 critical value per set, 0.039), plus per-replicate
+    laws per set and the pooled KS over all sets."""
     import make_golden
 
     g = _fixture("c4_subset")
+    m = make_golden.C4_REPS
+    n = 65536
     kw = dict(BENCH_STORES[store], bin_kmax=64 if store == "bins" else 0)
-    r = engine_mod.run(make_golden.c4_subset_spec(reps_per_set=16384, **kw))
+    r = engine_mod.run(make_golden.c4_subset_spec(reps_per_set=n, **kw))
+    assert np.all(r.summaries["error"] == 0)
     gh = g["hist"].reshape(16, -1)
     assert _ks(r.hist.sum(axis=0), gh.sum(axis=0)) < KS_TOL
-    crit = _ks_crit(16384, 4096, 1e-4)
+    worst = 0.0
     for i in range(16):
-        assert _ks(r.hist[i], gh[i]) < crit, (i, make_golden.C4_SETS[i])
-        sa = r.summaries[i * 16384:(i + 1) * 16384]
-        sb = {f: g[f][i * 4096:(i + 1) * 4096] for f in ("nminus", "nplus", "iters")}
+        ks = _ks(r.hist[i], gh[i])
+        worst = max(worst, ks)
+        assert ks < KS_TOL, (i, make_golden.C4_SETS[i], ks)
+        sa = r.summaries[i * n:(i + 1) * n]
+        sb = {f: g[f][i * m:(i + 1) * m] for f in ("nminus", "nplus", "iters")}
         _per_replicate_laws(sa, sb, 1e-5)
+    print(f"C4 subset ({store}): worst per-set KS {worst:.5f}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("store", sorted(BENCH_STORES))
+def test_c3_halved_cap_ks_against_reference_semantics(engine_mod, store):
+    """The other plausible reading of sosa's cell cap: the reference's BirthDeath
+    duplicates its population vector [n-, n+, n-, n+] (src/process.rs:339-344), so a cap tested against its sum
+    stops at n- + n+ >= max_cells / 2. Under ECDNA_FLAG_BD_CAP_COMPAT the engine (bench settings otherwise: C3 at
+    2^20 replicates, f64 time) matches the reference-semantics fixture made under the same reading: pooled KS
+    < 0.01 and per-replicate laws."""
+    import make_golden
+
+    g = _fixture("c3cap")
+    kw = dict(BENCH_STORES[store], bin_kmax=32 if store == "bins" else 0)
+    kw["flags"] |= abi.FLAG_BD_CAP_COMPAT
+    r = engine_mod.run(make_golden.c3_spec(n=1 << 20, **kw))
+    _invariants(r, make_golden.c3_spec())
+    full = r.summaries["stop_reason"] == abi.STOP_MAX_CELLS
+    assert np.all((r.summaries["nminus"] + r.summaries["nplus"])[full] == 5_000)
+    assert _ks(r.hist[0], g["hist"][0]) < KS_TOL
+    _per_replicate_laws(r.summaries, g, 1e-4)
 
 
 @pytest.mark.gpu
@@ -352,7 +380,7 @@ def test_c5_shaped_ks_against_reference_semantics(engine_mod, store):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["c3", "c4_subset", "c5_shaped"])
+@pytest.mark.parametrize("name", ["c3", "c4_subset", "c5_shaped", "c3cap"])
 def test_reference_draws_reproduce_bd_fixtures_seed_for_seed(engine_mod, name):
     """ECDNA_FLAG_REFERENCE_DRAWS (the Rust reference's draw structure) on the fixtures' exact configurations
     and replicate ids: every replicate's final n-, n+, events and stop reason, and the pooled histograms,
@@ -360,7 +388,9 @@ def test_reference_draws_reproduce_bd_fixtures_seed_for_seed(engine_mod, name):
     import make_golden
 
     spec = {"c3": make_golden.c3_spec, "c4_subset": make_golden.c4_subset_spec,
-            "c5_shaped": make_golden.c5_shaped_spec}[name](flags=abi.FLAG_REFERENCE_DRAWS)
+            "c5_shaped": make_golden.c5_shaped_spec,
+            "c3cap": lambda **kw: make_golden.c3_spec(**{**kw, "flags": kw["flags"] | abi.FLAG_BD_CAP_COMPAT})}[name](
+        flags=abi.FLAG_REFERENCE_DRAWS)
     g = _fixture(name)
     r = engine_mod.run(spec)
     np.testing.assert_array_equal(r.hist.reshape(-1), g["hist"].reshape(-1))

@@ -31,6 +31,9 @@ def host():
                                   C.c_size_t]
     L.ecdna_host_load.argtypes = [C.c_char_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
     L.ecdna_host_load.restype = C.c_int64
+    L.ecdna_host_subsample_reference.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
+                                                 C.c_uint64, C.POINTER(C.c_uint64), C.c_void_p,
+                                                 C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     return L
 
 
@@ -40,7 +43,7 @@ def test_host_library_exports_every_declared_symbol(host):
     with open(os.path.join(REPO, "include", "ecdna_host.h")) as f:
         text = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
     names = sorted(set(re.findall(r"\b(ecdna_host_\w+)\s*\(", text)))
-    assert len(names) == 6
+    assert len(names) == 7
     for n in names:
         assert hasattr(host, n), f"libecdna_host.so does not export {n}"
 
@@ -264,5 +267,163 @@ def test_cli_draws_option(host):
     assert dry()["draws"] == "philox"
     d = dry("--draws", "reference")
     assert (d["draws"], d["cell_store"]) == ("reference", "rows")  # the reference's draws need the row store
-    out = subprocess.run([CLI, "--dry-run", "--draws", "chacha", "/tmp/ecdna_out"], capture_output=True, text=True)
-    assert out.returncode != 0
+    assert dry("--draws", "reference", "--cell-store", "rows")["cell_store"] == "rows"
+    for bad in (["--draws", "chacha"], ["--draws", "reference", "--cell-store", "bins"],
+                ["--draws", "reference", "--bin-kmax", "256"]):  # an explicit bin-store option is refused, not dropped
+        out = subprocess.run([CLI, "--dry-run", *bad, "/tmp/ecdna_out"], capture_output=True, text=True)
+        assert out.returncode == 2 and "error" in out.stderr, bad
+
+
+# ---- end-of-run subsampling under the reference's draws (ecdna_host_subsample_reference): the replicate's ChaCha8
+# stream continued (src/main.rs:110-123), ecdna-lib 3.0.2 into_subsampled reconstructed as rand 0.8.5
+# SliceRandom::choose_multiple (seq::index::sample). Three restatements must agree: the host (product), the oracle
+# (oracle_compat_subsample) and the pure-Python one below (which reads the oracle's sequential ChaCha8 words, so it
+# also pins the seek to a word position).
+
+def _index_sample_py(next_u32, length, amount):
+    """rand 0.8.5 seq::index::sample for length < 2^32 (its algorithm choice in f32 and each algorithm's draws)."""
+    f32 = np.float32
+
+    def incl(lo, hi):  # UniformInt<u32>::sample_single_inclusive
+        rng_ = (hi - lo + 1) & 0xFFFFFFFF
+        zone = ((rng_ << (32 - rng_.bit_length())) & 0xFFFFFFFF) - 1
+        while True:
+            m = next_u32() * rng_
+            if (m & 0xFFFFFFFF) <= zone:
+                return lo + (m >> 32)
+
+    def uniform(n):  # Uniform::new(0, n).sample
+        zone = 0xFFFFFFFF - ((2**32 - n) % n)
+        while True:
+            m = next_u32() * n
+            if (m & 0xFFFFFFFF) <= zone:
+                return m >> 32
+
+    j = 0 if length < 500_000 else 1
+    if amount < 163:
+        c0, c1 = (f32(1.6), f32(8.0) / f32(45.0)), (f32(10.0), f32(70.0) / f32(9.0))
+        a = f32(amount)
+        alg = "inplace" if amount > 11 and f32(length) < (c1[j] + c0[j] * a) * a else "floyd"
+    else:
+        c = (f32(270.0), f32(330.0) / f32(9.0))
+        alg = "inplace" if f32(length) < c[j] * f32(amount) else "rejection"
+    if alg == "floyd":
+        idx = []
+        for jj in range(length - amount, length):
+            t = incl(0, jj)
+            if t not in idx:
+                idx.append(t)
+            elif amount < 50:  # the fully shuffled variant: j goes in before t
+                idx.insert(idx.index(t), jj)
+            else:
+                idx.append(jj)
+        if amount >= 50:
+            for i in range(amount - 1, 0, -1):
+                k = incl(0, i)
+                idx[i], idx[k] = idx[k], idx[i]
+    elif alg == "inplace":
+        allv = list(range(length))
+        for i in range(amount):
+            k = incl(i, length - 1)
+            allv[i], allv[k] = allv[k], allv[i]
+        idx = allv[:amount]
+    else:
+        idx, seen = [], set()
+        for _ in range(amount):
+            pos = uniform(length)
+            while pos in seen:
+                pos = uniform(length)
+            seen.add(pos)
+            idx.append(pos)
+    return alg, idx
+
+
+# (cells, nminus, amount): Floyd below 12, Floyd with the final shuffle (>= 50), in place, rejection (>= 163 of
+# a long row), the whole distribution (amount clamped to the cells), and the N- cells only
+SUBSAMPLE_CASES = [(300, 20, 5), (300, 20, 11), (12, 3, 11), (40, 0, 30), (2000, 100, 60), (3000, 0, 120), (400, 50, 300), (60000, 1000, 200),
+                   (30, 10, 100), (0, 40, 7), (1000, 0, 1000)]
+
+
+@pytest.mark.parametrize("n_plus,nminus,amount", SUBSAMPLE_CASES)
+def test_subsample_reference_host_oracle_python_agree(host, oracle_mod, n_plus, nminus, amount):
+    rng = np.random.default_rng(n_plus + amount)
+    nplus = rng.integers(1, 90, max(n_plus, 1)).astype(np.uint16)[:n_plus]
+    seed, stream = 42, 420 + 3
+    for start in (0, 1, 63, 64, 1000):  # word positions: fresh, odd, a 4-block buffer boundary, mid-stream
+        wh = C.c_uint64(start)
+        out = np.zeros(max(1, n_plus), np.uint16)
+        onp, onm = C.c_uint64(), C.c_uint64()
+        assert host.ecdna_host_subsample_reference(nplus.ctypes.data if n_plus else None, n_plus, nminus, amount,
+                                                   seed, stream, C.byref(wh), out.ctypes.data, C.byref(onp),
+                                                   C.byref(onm)) == 0
+        cells, wo = oracle_mod.compat_subsample(nplus, nminus, amount, seed, stream, start)
+        assert wh.value == wo
+        assert sorted(out[: onp.value].tolist()) == sorted(int(c) for c in cells if c) and onm.value == int(
+            np.sum(cells == 0))
+        assert onp.value + onm.value == min(amount, n_plus + nminus)
+        ch = oracle_mod.ChaCha(seed, stream)
+        for _ in range(start):
+            ch.next_u32()
+        used = [0]
+
+        def nxt():
+            used[0] += 1
+            return ch.next_u32()
+
+        alg, idx = _index_sample_py(nxt, n_plus + nminus, min(amount, n_plus + nminus))
+        want = [0 if i < nminus else int(nplus[i - nminus]) for i in idx]
+        assert cells.tolist() == want, alg
+        assert wo == start + used[0]
+
+
+def test_subsample_reference_chains_words(host, oracle_mod):
+    """Consecutive subsamples of one replicate continue the stream where the previous one stopped (the reference's
+    `for nb_cells in samples` loop reuses one rng): the word position advances by exactly the words drawn."""
+    nplus = np.arange(1, 501, dtype=np.uint16)
+    w = 777
+    for amount in (10, 100, 200):
+        _, w2 = oracle_mod.compat_subsample(nplus, 20, amount, 7, 71, w)
+        assert w2 > w
+        wh = C.c_uint64(w)
+        out = np.zeros(500, np.uint16)
+        onp, onm = C.c_uint64(), C.c_uint64()
+        host.ecdna_host_subsample_reference(nplus.ctypes.data, 500, 20, amount, 7, 71, C.byref(wh), out.ctypes.data,
+                                            C.byref(onp), C.byref(onm))
+        assert wh.value == w2
+        w = w2
+
+
+def test_oracle_compat_reports_stream_positions(oracle_mod):
+    """The compat oracle's per-replicate stream position: a replicate that drew nothing stands at 0; a pure-birth
+    replicate from one cell to 2 cells drew exactly one Exp1 (two words per next_u64 unless the ziggurat rejects)
+    plus its segregation and pick words; positions grow with the run."""
+    from ecdna_evo_amd import abi
+
+    spec = abi.RunSpec(seed=5, n_replicates=64, max_cells=200, flags=0)
+    r = oracle_mod.run(spec, mode="compat")
+    assert r.rng_words.shape == (64,) and np.all(r.rng_words > 0)
+    assert np.all(r.rng_words % 1 == 0)
+    big = oracle_mod.run(abi.RunSpec(seed=5, n_replicates=64, max_cells=400, flags=0), mode="compat")
+    assert np.all(big.rng_words >= r.rng_words)  # the same streams, run further
+
+
+def test_rendezvous_all_or_none(tmp_path):
+    """the --pooled rendezvous with the RCCL reduction stubbed (tests/native/rendezvous_check.cpp): all
+    shards OK -> every thread runs the collective; one shard failing -> none does, the failed one keeps its own error
+    and the others report the peer failure (ecdna::host::kPeerFailed), never hanging."""
+    exe = tmp_path / "rendezvous_check"
+    src = os.path.join(REPO, "tests", "native", "rendezvous_check.cpp")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-pthread", "-I", os.path.join(REPO, "ecdna-evo_amd", "host"), src,
+                    "-o", str(exe)], check=True)
+
+    def run(flags):
+        out = subprocess.run([str(exe), flags], capture_output=True, text=True, timeout=30, check=True).stdout
+        calls, rcs = out.strip().split()
+        return int(calls.split("=")[1]), [int(x) for x in rcs.split("=")[1].split(",")]
+
+    assert run("1") == (1, [0])
+    assert run("1111") == (4, [0, 0, 0, 0])
+    calls, rc = run("1101")
+    assert calls == 0 and rc == [-1000, -1000, -2, -1000]
+    calls, rc = run("0000")
+    assert calls == 0 and rc == [-2, -2, -2, -2]

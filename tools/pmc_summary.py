@@ -78,6 +78,8 @@ def main(src, tag):
                       "applies to 16-B/lane coalesced reads, reproduced by the calibration stream_load_x4 "
                       "ratio 0.5); on this access shape one random 2-B load = one 64-B read request and one "
                       "random 2-B store = one 32-B write request (calibration file)",
+        # the kernel instance the bench line timed (bench.py config.instance, ABI v7 ecdna_ssa_ctx_instance)
+        "instance": bench["config"].get("instance"),
         "launch": {k: st[k] for k in ("VGPR_Count", "SGPR_Count", "LDS_Block_Size", "Grid_Size")},
         "sq": {k: st[k] for k in st if k.startswith("SQ_")},
         "ssa_hist": pmc.get("ssa_hist"),
