@@ -62,10 +62,11 @@ InitOfSet init_of_set(const ecdna_ssa_params_t* p, uint64_t s) {
 int validate(const ecdna_ssa_params_t* p) {
     if (!p) return fail(ECDNA_E_INVALID, "params is NULL");
     if (!p->rates || p->n_param_sets == 0) return fail(ECDNA_E_INVALID, "rates/n_param_sets");
-    for (uint32_t s = 0; s < p->n_param_sets; ++s) {  // (the steppers' time-step division relies on it)
+    for (uint32_t s = 0; s < p->n_param_sets; ++s) {  // (the steppers' f32 time-step division relies on it)
         const ecdna_rates_t& r = p->rates[s];
         for (const float x : {r.b0, r.b1, r.d0, r.d1})
-            if (!(x >= 0.f && x <= FLT_MAX)) return fail(ECDNA_E_INVALID, "rates must be finite and >= 0");
+            if (!(x == 0.f || (x >= 0x1p-60f && x <= 0x1p60f)))
+                return fail(ECDNA_E_INVALID, "rates must be 0 or in [2^-60, 2^60]");
     }
     if (p->reps_per_set == 0) return fail(ECDNA_E_INVALID, "reps_per_set must be >= 1");
     if (p->hist_bins < 2 || p->hist_bins > ecdna::kMaxHistBins)
@@ -530,9 +531,12 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
         // (auto only without f32 time and the event hash: that variant spills 12 B at 128 VGPRs)
         const bool k64u16 = c->bin_k == 64 && !c->bin_c32;
         const bool tf0 = (p->flags & (ECDNA_FLAG_TIME_F32 | ECDNA_FLAG_EVENT_HASH)) == 0;
-        // Where the max-ILP build keeps the default's occupancy (LDS bounds both: K = 64 / u32 at two
-        // workgroups per CU, K = 256; K = 64 / u16 at three) it is taken too: its schedule then costs no
-        // lanes (C5 whole, K = 64 / u32: 35.3 -> 34.1 s same-box).
+        // Where the max-ILP build keeps the default's occupancy (LDS bounds both: K = 32 / u32 and K = 64 / u32
+        // since the f32 draw mapping v6, K = 256) it is taken too: its schedule then costs no lanes (C3 78.3 ->
+        // 77.3 ms, C5 whole 31.9 -> 30.4 s, same box). With fewer than four replicates per lane of the default
+        // grid it is taken even at one workgroup per CU less (K = 64 / u16, 118 against 134 VGPRs since v6: the
+        // C4 8-GPU shard, two replicates per lane, 127 -> 119 ms), as the drain of the last replicates is
+        // latency-bound (profiles/r04d_v6_suite_and_sched_sweep.txt).
         int occ_def = 0, occ_ilp = 0;
         CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &occ_def, ecdna::bin_stepper_kernel(p->process, p->segregation, c->bin_k, c->bin_c32, p->flags, 0),
@@ -554,7 +558,7 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
             c->bin_ilp = 1;
         else if (k64u16 && (sched == 3 || (sched == 2 && tf0 && max_chunk >= 4ull * c->cus * 4u * ecdna::kStepperBlock)))
             c->bin_ilp = 2;
-        else if (sched == 2 && occ_ilp >= occ_def)
+        else if (sched == 2 && (occ_ilp >= occ_def || max_chunk < 4ull * (uint64_t)occ_def * c->cus * c->stepper_block))
             c->bin_ilp = 1;
         else
             c->bin_ilp = 0;

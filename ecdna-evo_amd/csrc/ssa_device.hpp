@@ -106,17 +106,59 @@ __device__ __forceinline__ uint4 philox_event(uint32_t e, const PhiloxEventPre& 
     return c;
 }
 
-// -ln((w + 0.5) 2^-32), draw mapping v2: d = w + 0.5 = m 2^ex with m in [0.5, 1); the
-// top 7 fraction bits j of m pick {C, LN} = {1/mid_j, ln mid_j} (ssa_logtab.h, staged in LDS), r =
-// m C - 1 (|r| <= 2^-8, the subtraction exact), ln(1 + r) by a degree-7 series in explicit fmas, and
-// -ln u = -(LN + ln(1 + r) + (ex - 32) ln 2). oracle_softlog_neg (oracle/ssa_oracle.c) performs the
-// same IEEE operations in the same order, so CPU and GPU agree bit for bit.
-// v_fma_f64 in its 3-address (VOP3) form: left to itself the compiler picks the 2-address v_fmac_f64
-// plus a v_mov_b64 of the addend for each Horner step. Same correctly rounded fma.
-__device__ __forceinline__ double fma3(double a, double b, double c) {
-    double d;
-    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-    return d;
+// -ln u for u = ((w >> 9) + 0.5) 2^-23, draw mapping v6, in f32: d = (w >> 8) | 1 is odd and below
+// 2^24, so (float)d is exact, = m 2^ex with m in [0.5, 1) and u = d 2^-24; the top 7 fraction bits j of m pick
+// {C, LN} = {RN32(1/mid_j), RN32(-ln C)} (ssa_logtab.h, staged in LDS; LN is the log of the stored C, so ln m =
+// ln(m C) + LN exactly whatever C's rounding; entry 127 = {1, 0}, so u -> 1 keeps its relative accuracy);
+// r = fma(m, C, -1) (|r| <= 2^-8); ln(1 + r) by a degree-4 series in explicit fmas (truncation |r|^5 / 5 <= 2^-42);
+// -ln u = -(LN + ln(1 + r) + k ln 2), k = ex - 24 in [-23, 0], with ln 2 as an exact head (k LN2_HI is exact) and a
+// tail. oracle_softlog_neg (oracle/ssa_oracle.c) performs the same IEEE f32 operations in the same order, so CPU
+// and GPU agree bit for bit. (v2-v5 formed the same function in f64 from all 32 bits of w: MI355X issues f64
+// arithmetic at half the f32 rate, and the stepper is issue-bound.)
+struct SoftlogParts {
+    float2 cl;
+    float m;
+    int k;
+};
+
+// the table load (begin) and the arithmetic after it (end), so that a loop can issue the load one iteration ahead
+__device__ __forceinline__ SoftlogParts softlog_begin(uint32_t w, const float2* tab) {
+    const uint32_t bits = __float_as_uint((float)((w >> 8) | 1u));  // exact
+    SoftlogParts p;
+    p.k = (int)(bits >> 23) - 150;                                 // ex - 24, ex = biased exponent - 126
+    p.m = __uint_as_float((bits & 0x007fffffu) | 0x3f000000u);      // m in [0.5, 1)
+    p.cl = tab[(bits >> 16) & 127u];
+    return p;
+}
+
+__device__ __forceinline__ float softlog_end(const SoftlogParts& p) {
+    const float r = fmaf(p.m, p.cl.x, -1.0f);
+    float q = fmaf(r, -0.25f, 0x1.555556p-2f);  // -1/4, RN32(1/3)
+    q = fmaf(r, q, -0.5f);
+    const float l = fmaf(r * r, q, r);  // ln(1 + r)
+    const float kf = (float)p.k;
+    return -fmaf(kf, ECDNA_LN2_HI, fmaf(kf, ECDNA_LN2_LO, p.cl.y + l));
+}
+
+__device__ __forceinline__ float softlog_neg(uint32_t w, const float2* tab) { return softlog_end(softlog_begin(w, tab)); }
+
+// The channel's uniform, draw mapping v6: ((w >> 9) + 0.5) 2^-23, formed exactly by one fma. Below 1 - 2^-24, so
+// target = u a0 (RN32) stays below a0 and a last channel of zero propensity is never drawn.
+__device__ __forceinline__ float chan_u(uint32_t w) { return fmaf((float)(w >> 9), 0x1p-23f, 0x1p-24f); }
+
+// n / d, the correctly rounded IEEE f32 quotient (the oracle's C division), for operands in the stepper's range.
+// LLVM lowers an f32 divide to v_div_scale x2, v_rcp_f32, the Newton step, the quotient and two residual
+// corrections, v_div_fmas and v_div_fixup; the scales, the scale flag of v_div_fmas and the fixup only act when an
+// operand, the quotient or a residual is near the denormal or overflow range, or on zero / inf / NaN divisors. The
+// time step divides a soft log in [2^-24, 16.7] by a total propensity in [2^-60, 2^94] (every rate 0 or in
+// [2^-60, 2^60], which ecdna_ssa_ctx_create requires; u32 populations; a0 > 0), so every intermediate is a normal
+// f32 and the same rcp / fma sequence without them yields the same bits.
+__device__ __forceinline__ float div_in_range(float n, float d) {
+    const float r0 = __builtin_amdgcn_rcpf(d);
+    const float r1 = fmaf(fmaf(-d, r0, 1.0f), r0, r0);
+    const float q0 = n * r1;
+    const float q1 = fmaf(fmaf(-d, q0, n), r1, q0);
+    return fmaf(fmaf(-d, q1, n), r1, q1);
 }
 
 // 32 x 32 -> 64-bit product as one v_mad_u64_u32 (the compiler widens a u32 * u64 into two)
@@ -126,61 +168,12 @@ __device__ __forceinline__ uint64_t mul_u32_wide(uint32_t a, uint32_t b) {
     return d;
 }
 
-// softlog_neg in two halves: the table load (begin) and the arithmetic after it (end), so that a loop can
-// issue the load one iteration ahead and overlap its latency
-struct SoftlogParts {
-    double2 cl;
-    double m;
-    int ex;
-};
-
-__device__ __forceinline__ SoftlogParts softlog_begin(uint32_t w, const double2* tab) {
-    const double d = (double)w + 0.5;  // exact
-    const uint64_t bits = (uint64_t)__double_as_longlong(d);
-    const uint32_t hi = (uint32_t)(bits >> 32);
-    SoftlogParts p;
-    p.ex = (int)(hi >> 20) - 1022;
-    p.m = __longlong_as_double((long long)((bits & 0x000fffffffffffffull) | (1022ull << 52)));
-    p.cl = tab[(hi >> 13) & 127u];
-    return p;
-}
-
-__device__ __forceinline__ double softlog_end(const SoftlogParts& p) {
-    const double r = p.m * p.cl.x - 1.0;
-    double q = fma3(r, 0x1.2492492492492p-3, -0x1.5555555555555p-3);  // 1/7, -1/6
-    q = fma3(r, q, 0x1.999999999999ap-3);                                // 1/5
-    q = fma3(r, q, -0x1p-2);                                             // -1/4
-    q = fma3(r, q, 0x1.5555555555555p-2);                                // 1/3
-    q = fma3(r, q, -0x1p-1);                                             // -1/2
-    const double l = fma(r * r, q, r);                                  // ln(1 + r)
-    return -fma((double)(p.ex - 32), 0x1.62e42fefa39efp-1, p.cl.y + l);
-}
-
-__device__ __forceinline__ double softlog_neg(uint32_t w, const double2* tab) {
-    return softlog_end(softlog_begin(w, tab));
-}
-
-// n / d, the correctly rounded IEEE quotient (the oracle's C division), for operands in the stepper's
-// range. LLVM lowers an f64 divide to v_div_scale x2, v_rcp_f64, two Newton steps, the quotient and its
-// residual, v_div_fmas and v_div_fixup; the scales, the scale flag of v_div_fmas and the fixup only act
-// when an operand or the quotient is near the denormal or overflow range, or on zero / inf / NaN
-// divisors. The time step divides a soft log in [2^-33, 23] (or 0) by a total propensity in
-// [2^-200, 2^162] (finite non-negative f32 rates, ecdna_ssa_ctx_create; u32 populations; a0 > 0), so
-// they are identities there and the same rcp / fma sequence without them yields the same bits.
-__device__ __forceinline__ double div_in_range(double n, double d) {
-    const double r0 = __builtin_amdgcn_rcp(d);
-    const double r1 = fma(r0, fma(-d, r0, 1.0), r0);
-    const double r2 = fma(r1, fma(-d, r1, 1.0), r1);
-    const double q = n * r2;
-    return fma(fma(-d, q, n), r2, q);
-}
-
 // The log table in constant memory; each workgroup stages it into LDS (divergent per-lane index).
-__constant__ const double kLogTab[2 * ECDNA_LOGTAB_N] = ECDNA_LOGTAB_INIT;
+__constant__ const float kLogTab[2 * ECDNA_LOGTAB_N] = ECDNA_LOGTAB_INIT;
 
-__device__ __forceinline__ void stage_logtab(double2* lds) {
+__device__ __forceinline__ void stage_logtab(float2* lds) {
     for (uint32_t i = threadIdx.x; i < ECDNA_LOGTAB_N; i += blockDim.x)
-        lds[i] = make_double2(kLogTab[2 * i], kLogTab[2 * i + 1]);
+        lds[i] = make_float2(kLogTab[2 * i], kLogTab[2 * i + 1]);
     __syncthreads();
 }
 

@@ -48,7 +48,7 @@ constexpr uint32_t kFlush = 16;
 template <bool BD, int SEG, bool WIN>
 __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a) {
     __shared__ uint16_t win[WIN ? kWin + 1 : 1][kStepperBlock];  // + 1 spare row
-    __shared__ double2 logtab[ECDNA_LOGTAB_N];
+    __shared__ float2 logtab[ECDNA_LOGTAB_N];
     stage_logtab(logtab);
     const uint32_t tid = threadIdx.x;
     const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
@@ -190,23 +190,20 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
             }
         }
 
-        // propensities rate_i * population_i over [n-, n+(, n-, n+)]
-        const double pa = (double)b0 * (double)nm;
-        const double pb = (double)b1 * (double)np;
-        const double cA = pa;
-        const double cB = cA + pb;
-        double cC = cB, a0 = cB;
+        // propensities rate_i * population_i over [n-, n+(, n-, n+)], f32 (draw mapping v6)
+        const float fnm = (float)nm, fnp = (float)np;
+        const float cA = b0 * fnm;
+        const float cB = cA + b1 * fnp;
+        float cC = cB, a0 = cB;
         if (BD) {
-            const double pc = (double)d0 * (double)nm;
-            const double pd = (double)d1 * (double)np;
-            cC = cB + pc;
-            a0 = cC + pd;
+            cC = cB + d0 * fnm;
+            a0 = cC + d1 * fnp;
         }
 
         // stop checks, in the order of DESIGN.md §3.1 (selects, last write = first check)
         {
             const bool t_over = f32t ? (t32 >= a.max_time32) : (t >= a.max_time);
-            uint32_t s = (a0 > 0.0) ? 0u : (uint32_t)ECDNA_STOP_ABSORBING;
+            uint32_t s = (a0 > 0.0f) ? 0u : (uint32_t)ECDNA_STOP_ABSORBING;
             s = t_over ? (uint32_t)ECDNA_STOP_MAX_TIME : s;
             s = ((uint64_t)nm + np >= a.stop_cells) ? (uint32_t)ECDNA_STOP_MAX_CELLS : s;
             s = (e >= a.max_iter) ? (uint32_t)ECDNA_STOP_MAX_ITER : s;
@@ -250,7 +247,7 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
 
         const uint32_t rid_lo = (uint32_t)rid, rid_hi = (uint32_t)(rid >> 32);
         const uint4 w = philox4x32_10(make_uint4(e, 0u, rid_lo, rid_hi), k0, k1);
-        const double target = (((double)w.y + 0.5) * 0x1p-32) * a0;
+        const float target = chan_u(w.y) * a0;
         uint32_t ch;
         if (BD)
             ch = target < cA ? 0u : (target < cB ? 1u : (target < cC ? 2u : 3u));
@@ -350,7 +347,7 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
         }
 
         // waiting time
-        const double tau = div_in_range(softlog_neg(w.x, logtab), a0);
+        const float tau = div_in_range(softlog_neg(w.x, logtab), a0);
 
         uint64_t x = ch;
         if (ch == 1u) {
@@ -388,9 +385,9 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
         if (BD) n_dm += ch == 2u ? 1u : 0u;
         e += 1;
         if (f32t)
-            t32 = t32 + (float)tau;
+            t32 = t32 + tau;
         else
-            t = t + tau;
+            t = t + (double)tau;
         if (hash_on) h = (h ^ x) * kFnvPrime;
     }
 }
@@ -628,7 +625,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
     constexpr uint32_t K = L::kK;
     __shared__ uint4 cnt_v[L::kBinVecs][BLK];  // bin counters
     __shared__ uint4 sum_v[L::kSumVecs][BLK];  // group sums
-    __shared__ double2 logtab[ECDNA_LOGTAB_N];
+    __shared__ float2 logtab[ECDNA_LOGTAB_N];
     stage_logtab(logtab);
     const uint32_t tid = threadIdx.x;
     const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
@@ -772,7 +769,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
     uint16_t* row = a.rows;
     uint32_t nm = 0, ns = 0, nb = 0;
     uint32_t sp0 = 0, sp1 = 0, nsp = 0;                 // spare stream words (draw mapping v3)
-    double rb0 = 0.0, rb1 = 0.0, rd0 = 0.0, rd1 = 0.0;  // the f32 rates, widened once per replicate
+    float rb0 = 0.f, rb1 = 0.f, rd0 = 0.f, rd1 = 0.f;  // the replicate's rates
     double t = 0.0;
     float t32 = 0.f;
     // Per-type event counts: only DeathNMinus (BD) and uneven splits are counted per event; the other
@@ -924,10 +921,10 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
             row = ra->rows + (uint64_t)i * ra->row_stride;
             const uint64_t set = rid / ra->reps_per_set;
             const float4 r = ra->rates[set];
-            rb0 = (double)r.x;
-            rb1 = (double)r.y;
-            rd0 = (double)r.z;
-            rd1 = (double)r.w;
+            rb0 = r.x;
+            rb1 = r.y;
+            rd0 = r.z;
+            rd1 = r.w;
             stop = 0;
             err = 0;
             if (kind == ROT_PARKED + 1u) {  // resume: the parker's stores, through the XCD's L2
@@ -1033,10 +1030,10 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
         // fast-forwarding, every iteration while it is (wave-uniform control: ballots at the loop top).
         if (BD && kFfMax && !a.n_snap && (ff_mode || (ff_tick & (ECDNA_FF_TEST_EVERY - 1u)) == 0u)) {
             const uint32_t npf = ns + nb;  // n+ is fixed during N- events
-            const double fpf = (double)npf;
-            const double pbf = rb1 * fpf, pdf = rd1 * fpf;
-            const double pm = rb0 * (double)nm + rd0 * (double)nm;
-            const bool heavy = active && pm * 8.0 >= (pm + pbf + pdf) * (double)ECDNA_FF_ENTER8;
+            const float fpf = (float)npf;
+            const float pbf = rb1 * fpf, pdf = rd1 * fpf;
+            const float pm = rb0 * (float)nm + rd0 * (float)nm;
+            const bool heavy = active && pm * 8.0f >= (pm + pbf + pdf) * (float)ECDNA_FF_ENTER8;  // (speed only)
             const uint32_t n_in = (uint32_t)__builtin_popcountll(__ballot(active));
             ff_mode = n_in != 0u && (uint32_t)__builtin_popcountll(__ballot(heavy)) * 8u >= n_in * ECDNA_FF_ENTER8;
             CYC_ADD(4, ff_mode ? 1u : 0u);
@@ -1075,16 +1072,13 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                 for (uint32_t q = 0; q < kFfMax; q += 2) {
                     if ((uint32_t)__builtin_popcountll(__ballot(go)) * 8u < n_in * ECDNA_FF_STAY8) break;  // (uniform)
                     CYC_ADD(5, 1);
-                    const double lg = softlog_end(lp);
+                    const float lg = softlog_end(lp);
                     // the helper's block and soft log (event e + 1) to the owner
-                    const uint64_t lgb = (uint64_t)__double_as_longlong(lg);
-                    const uint32_t lo2 = __builtin_amdgcn_permlane32_swap((uint32_t)lgb, (uint32_t)lgb, false, false)[1];
-                    const uint32_t hi2 =
-                        __builtin_amdgcn_permlane32_swap((uint32_t)(lgb >> 32), (uint32_t)(lgb >> 32), false, false)[1];
+                    const uint32_t lgb = __float_as_uint(lg);
+                    const float lg2 = __uint_as_float(__builtin_amdgcn_permlane32_swap(lgb, lgb, false, false)[1]);
                     const uint32_t y2 = __builtin_amdgcn_permlane32_swap(wb.y, wb.y, false, false)[1];
                     const uint32_t z2 = __builtin_amdgcn_permlane32_swap(wb.z, wb.z, false, false)[1];
                     const uint32_t w2 = __builtin_amdgcn_permlane32_swap(wb.w, wb.w, false, false)[1];
-                    const double lg2 = __longlong_as_double((long long)(((uint64_t)hi2 << 32) | lo2));
 #ifdef ECDNA_PAIR_CHECK
                     // (debug builds) the helper is still in step: its counter is the owner's e + 1. A helper that
                     // left early (EXEC at the loop top narrowed by a compiler change) would hand over stale words;
@@ -1096,42 +1090,42 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     constexpr bool pair_ok = true;
 #endif
                     const uint4 wa = wb;
-                    const double lga = lg;
+                    const float lga = lg;
                     // the next step's words (events e + 2, e + 3), off this step's chain
                     ctr += 2u;
                     wb = philox_event(ctr, hp, rk);
                     lp = softlog_begin(wb.x, logtab);
                     // event e (conditions as 0/1 words combined with bitwise ops: no short-circuit branches, so
                     // the step stays one basic block for the scheduler)
-                    const double fmA = (double)nm;
-                    const double cAA = rb0 * fmA;
-                    const double cBA = cAA + pbf;
-                    const double cCA = cBA + rd0 * fmA;
-                    const double a0A = cCA + pdf;
+                    const float fmA = (float)nm;
+                    const float cAA = rb0 * fmA;
+                    const float cBA = cAA + pbf;
+                    const float cCA = cBA + rd0 * fmA;
+                    const float a0A = cCA + pdf;
                     const uint32_t overA = f32t ? (uint32_t)(t32 >= a.max_time32) : (uint32_t)(t >= a.max_time);
-                    const double targetA = fma3((double)wa.y, 0x1p-32, 0x1p-33) * a0A;
+                    const float targetA = chan_u(wa.y) * a0A;
                     const uint32_t chA = (uint32_t)(targetA >= cAA) + (uint32_t)(targetA >= cBA) +
                                          (uint32_t)(targetA >= cCA);
                     const uint32_t okA = (uint32_t)go & (uint32_t)(e < a.max_iter) & (uint32_t)(nm + npf < stop32) &
-                                         (overA ^ 1u) & (uint32_t)(a0A > 0.0) & (~chA & 1u);
+                                         (overA ^ 1u) & (uint32_t)(a0A > 0.0f) & (~chA & 1u);
                     const uint32_t nmB = nm + (uint32_t)(chA == 0u) - (uint32_t)(chA == 2u);
-                    const double tauA = div_in_range(lga, a0A);
-                    const double tB = t + tauA;
-                    const float t32B = t32 + (float)tauA;
+                    const float tauA = div_in_range(lga, a0A);
+                    const double tB = t + (double)tauA;
+                    const float t32B = t32 + tauA;
                     // event e + 1, from the state after e
-                    const double fmB = (double)nmB;
-                    const double cAB = rb0 * fmB;
-                    const double cBB = cAB + pbf;
-                    const double cCB = cBB + rd0 * fmB;
-                    const double a0B = cCB + pdf;
+                    const float fmB = (float)nmB;
+                    const float cAB = rb0 * fmB;
+                    const float cBB = cAB + pbf;
+                    const float cCB = cBB + rd0 * fmB;
+                    const float a0B = cCB + pdf;
                     const uint32_t overB = f32t ? (uint32_t)(t32B >= a.max_time32) : (uint32_t)(tB >= a.max_time);
-                    const double targetB = fma3((double)y2, 0x1p-32, 0x1p-33) * a0B;
+                    const float targetB = chan_u(y2) * a0B;
                     const uint32_t chB = (uint32_t)(targetB >= cAB) + (uint32_t)(targetB >= cBB) +
                                          (uint32_t)(targetB >= cCB);
                     const uint32_t okB = okA & (uint32_t)pair_ok & (uint32_t)(e + 1u < a.max_iter) & (uint32_t)(nmB + npf < stop32) &
-                                         (overB ^ 1u) & (uint32_t)(a0B > 0.0) & (~chB & 1u);
+                                         (overB ^ 1u) & (uint32_t)(a0B > 0.0f) & (~chB & 1u);
                     const uint32_t nmC = nmB + (uint32_t)(chB == 0u) - (uint32_t)(chB == 2u);
-                    const double tauB = div_in_range(lg2, a0B);
+                    const float tauB = div_in_range(lg2, a0B);
                     // commit. An N- event consumes no stream word after w1, so its spare update pushes w2 and
                     // w3 onto the stack and leaves exactly those two (spares_update with used = 0).
                     const bool cA = okA != 0u, cB = okB != 0u;
@@ -1142,9 +1136,9 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     n_dm += (okA & (uint32_t)(chA == 2u)) + (okB & (uint32_t)(chB == 2u));
                     e += okA + okB;
                     if (f32t)
-                        t32 = cB ? t32B + (float)tauB : (cA ? t32B : t32);
+                        t32 = cB ? t32B + tauB : (cA ? t32B : t32);
                     else
-                        t = cB ? tB + tauB : (cA ? tB : t);
+                        t = cB ? tB + (double)tauB : (cA ? tB : t);
                     if (hash_on) {
                         const uint64_t hA = (h ^ (uint64_t)chA) * kFnvPrime;
                         const uint64_t hB = (hA ^ (uint64_t)chB) * kFnvPrime;
@@ -1159,31 +1153,31 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     if ((uint32_t)__builtin_popcountll(__ballot(go)) * 8u < n_in * ECDNA_FF_STAY8) break;  // (uniform)
                     CYC_ADD(5, 1);
                     if (go) {
-                        const double fm2 = (double)nm;
-                        const double cA2 = rb0 * fm2;
-                        const double cB2 = cA2 + pbf;
-                        const double cC2 = cB2 + rd0 * fm2;
-                        const double a02 = cC2 + pdf;
+                        const float fm2 = (float)nm;
+                        const float cA2 = rb0 * fm2;
+                        const float cB2 = cA2 + pbf;
+                        const float cC2 = cB2 + rd0 * fm2;
+                        const float a02 = cC2 + pdf;
                         const bool t_over2 = f32t ? (t32 >= a.max_time32) : (t >= a.max_time);
-                        if ((e >= a.max_iter) || nm + npf >= stop32 || t_over2 || !(a02 > 0.0)) {
+                        if ((e >= a.max_iter) || nm + npf >= stop32 || t_over2 || !(a02 > 0.0f)) {
                             go = false;
                         } else {
                             const uint4 w2 = philox_event(e, pre, rk);
-                            const double target2 = fma3((double)w2.y, 0x1p-32, 0x1p-33) * a02;
+                            const float target2 = chan_u(w2.y) * a02;
                             const uint32_t ch2 = (target2 >= cA2 ? 1u : 0u) + (target2 >= cB2 ? 1u : 0u) +
                                                  (target2 >= cC2 ? 1u : 0u);
                             if (ch2 & 1u) {
                                 go = false;
                             } else {
-                                const double tau2 = div_in_range(softlog_neg(w2.x, logtab), a02);
+                                const float tau2 = div_in_range(softlog_neg(w2.x, logtab), a02);
                                 spares_update(0u, w2.z, w2.w, sp0, sp1, nsp);
                                 nm = nm + (ch2 == 0u ? 1u : 0u) - (ch2 == 2u ? 1u : 0u);
                                 n_dm += ch2 == 2u ? 1u : 0u;
                                 e += 1;
                                 if (f32t)
-                                    t32 = t32 + (float)tau2;
+                                    t32 = t32 + tau2;
                                 else
-                                    t = t + tau2;
+                                    t = t + (double)tau2;
                                 if (hash_on) h = (h ^ (uint64_t)ch2) * kFnvPrime;
                             }
                         }
@@ -1198,11 +1192,11 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
         PATH_STAT_LANES(1);
         const uint32_t np = ns + nb;
 
-        // propensities rate_i * population_i over [n-, n+(, n-, n+)]
-        const double fm = (double)nm, fp = (double)np;
-        const double cA = rb0 * fm;
-        const double cB = cA + rb1 * fp;
-        double cC = cB, a0 = cB;
+        // propensities rate_i * population_i over [n-, n+(, n-, n+)], f32 (draw mapping v6)
+        const float fm = (float)nm, fp = (float)np;
+        const float cA = rb0 * fm;
+        const float cB = cA + rb1 * fp;
+        float cC = cB, a0 = cB;
         if (BD) {
             cC = cB + rd0 * fm;
             a0 = cC + rd1 * fp;
@@ -1210,7 +1204,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
         // stop checks: one test here, the reason only when a lane stops
         const bool t_over = f32t ? (t32 >= a.max_time32) : (t >= a.max_time);
         const bool cells_over = nm + np >= stop32;  // (u32: cell counts stay below 2^32)
-        if ((e >= a.max_iter) || cells_over || t_over || !(a0 > 0.0)) {
+        if ((e >= a.max_iter) || cells_over || t_over || !(a0 > 0.0f)) {
             stop = (e >= a.max_iter) ? (uint32_t)ECDNA_STOP_MAX_ITER
                    : cells_over     ? (uint32_t)ECDNA_STOP_MAX_CELLS
                    : t_over         ? (uint32_t)ECDNA_STOP_MAX_TIME
@@ -1239,8 +1233,8 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
             const uint4 w = philox_event(e, pre, rk);
             // direct method: the channel is the number of cumulative propensities <= target (the first i
             // with target < c_i; the c_i are non-decreasing)
-            // (w1 + 0.5) 2^-32 formed exactly by one fma (the same value the oracle's add and scaling give)
-            const double target = fma3((double)w.y, 0x1p-32, 0x1p-33) * a0;
+            // ((w1 >> 9) + 0.5) 2^-23 formed exactly by one fma (chan_u), times a0 (RN32)
+            const float target = chan_u(w.y) * a0;
             uint32_t ch = (target >= cA ? 1u : 0u);
             if (BD) ch += (target >= cB ? 1u : 0u) + (target >= cC ? 1u : 0u);
             const bool nplus_ev = (ch & 1u) != 0;  // ProliferateNPlus or DeathNPlus: a cell is picked
@@ -1367,7 +1361,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                 stop = ECDNA_STOP_ERROR;
                 active = false;
             } else {
-                const double tau = div_in_range(softlog_neg(w.x, logtab), a0);
+                const float tau = div_in_range(softlog_neg(w.x, logtab), a0);
                 CYC_MARK(13);
 
                 const uint32_t ns_old = ns;
@@ -1408,9 +1402,9 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                 if (BD) n_dm += ch == 2u ? 1u : 0u;
                 e += 1;
                 if (f32t)
-                    t32 = t32 + (float)tau;
+                    t32 = t32 + tau;
                 else
-                    t = t + tau;
+                    t = t + (double)tau;
                 if (hash_on) {
                     const uint64_t x = (uint64_t)ch | (prolif ? ((uint64_t)k1v << 2) : 0ull) |
                                        (nplus_ev ? ((uint64_t)idx << 20) : 0ull);

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ECDNA_SSA_ABI_VERSION 7
+#define ECDNA_SSA_ABI_VERSION 8
 
 /* Process type — ProcessType (src/clap_app.rs:311-315); chosen as BirthDeath
  * when d0 > 0 or d1 > 0 (src/clap_app.rs:163-174, 194-200). */
@@ -127,8 +127,9 @@ typedef enum {
 #define ECDNA_E_COMM (-6)      /* RCCL error, or librccl.so.1 not loadable (multi-GPU reduction only) */
 
 /* Rates of one parameter set: ReactionRates([b0, b1, d0, d1]) (src/main.rs:67, 139). f32 as in Cli
- * (src/clap_app.rs:41-55). Each must be finite and >= 0 (else ECDNA_E_INVALID; the reference does not
- * check them). */
+ * (src/clap_app.rs:41-55). Each must be 0 or in [2^-60, 2^60] (else ECDNA_E_INVALID; the reference does not
+ * check them; ABI v8): the f32 propensities of draw mapping v6 (rate x population, u32 populations) then stay
+ * normal and finite, which the stepper's time-step division relies on. */
 typedef struct {
     float b0, b1, d0, d1;
 } ecdna_rates_t;

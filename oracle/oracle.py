@@ -46,7 +46,7 @@ def lib():
     L.oracle_philox4x32_10.argtypes = [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]
     L.oracle_philox4x32_10.restype = None
     L.oracle_softlog_neg.argtypes = [C.c_uint32]
-    L.oracle_softlog_neg.restype = C.c_double
+    L.oracle_softlog_neg.restype = C.c_float
     for fn in (L.oracle_run_philox, L.oracle_run_compat):
         fn.argtypes = [P(abi.Params), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int]
         fn.restype = C.c_int

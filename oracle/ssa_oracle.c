@@ -23,10 +23,11 @@
  * The draws follow the engine's mapping, not ChaCha8: see
  * ssa_compat.c for the reference-semantics samplers.
  *
- * Floating point: compile with -ffp-contract=off. Every f64 operation below is
- * a correctly rounded IEEE add/sub/mul/div in a fixed order, so the HIP kernel
- * (which spells the same operations with contraction disabled) reproduces the
- * times and channel picks bit for bit.
+ * Floating point: compile with -ffp-contract=off. Every f32 / f64 operation
+ * below is a correctly rounded IEEE add/sub/mul/div/fma in a fixed order (the
+ * propensities, channel and time step in f32, draw mapping v6; the clock in
+ * f64), so the HIP kernel (which spells the same operations with contraction
+ * disabled) reproduces the times and channel picks bit for bit.
  */
 #include "ssa_oracle.h"
 #include "ssa_logtab.h"
@@ -74,33 +75,35 @@ void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t
 
 /* -------------------------------------------------------------- soft log */
 
-/* -ln(u), u = (w + 0.5) * 2^-32: the engine's draw mapping v2. d = w + 0.5 (exact) =
- * m 2^ex with m in [0.5, 1); the top 7 fraction bits j of m select {C, LN} = {RN(1/mid_j), RN(ln mid_j)}
- * (ssa_logtab.h, tools/gen_logtab.py); r = m C - 1 (|r| <= 2^-8); ln(1 + r) by a degree-7 series in
- * explicit fma (C99 fma is the correctly rounded fused operation, like v_fma_f64); -ln u =
- * -(LN + ln(1 + r) + (ex - 32) ln 2). Fixed operation order. */
-static const double LOGTAB[2 * ECDNA_LOGTAB_N] = ECDNA_LOGTAB_INIT;
+/* -ln(u), u = ((w >> 9) + 0.5) * 2^-23: the engine's draw mapping v6, in f32. d = (w >> 8) | 1
+ * (odd, < 2^24: (float)d is exact) = m 2^ex with m in [0.5, 1) and u = d 2^-24; the top 7 fraction bits j of m
+ * select {C, LN} = {RN32(1/mid_j), RN32(ln mid_j)} (ssa_logtab.h, tools/gen_logtab.py); r = fma(m, C, -1)
+ * (|r| <= 2^-8); ln(1 + r) by a degree-4 series in explicit fmaf (C99 fmaf is the correctly rounded fused
+ * operation, like v_fma_f32); -ln u = -(LN + ln(1 + r) + k ln 2), k = ex - 24, ln 2 = LN2_HI + LN2_LO with k LN2_HI
+ * exact. Fixed operation order, float arithmetic only (FLT_EVAL_METHOD 0). */
+static const float LOGTAB[2 * ECDNA_LOGTAB_N] = ECDNA_LOGTAB_INIT;
 
-double oracle_softlog_neg(uint32_t w) {
-    const double d = (double)w + 0.5;
-    uint64_t bits;
+float oracle_softlog_neg(uint32_t w) {
+    const float d = (float)((w >> 8) | 1u);
+    uint32_t bits;
     memcpy(&bits, &d, sizeof bits);
-    const uint32_t hi = (uint32_t)(bits >> 32);
-    const int ex = (int)(hi >> 20) - 1022;
-    const uint64_t mb = (bits & 0x000fffffffffffffull) | (1022ull << 52);
-    double m;
+    const int k = (int)(bits >> 23) - 150;
+    const uint32_t mb = (bits & 0x007fffffu) | 0x3f000000u;
+    float m;
     memcpy(&m, &mb, sizeof m);
-    const uint32_t j = (hi >> 13) & 127u;
-    const double c = LOGTAB[2 * j], ln = LOGTAB[2 * j + 1];
-    const double r = m * c - 1.0;
-    double q = fma(r, 0x1.2492492492492p-3, -0x1.5555555555555p-3); /* 1/7, -1/6 */
-    q = fma(r, q, 0x1.999999999999ap-3);                               /* 1/5 */
-    q = fma(r, q, -0x1p-2);                                            /* -1/4 */
-    q = fma(r, q, 0x1.5555555555555p-2);                               /* 1/3 */
-    q = fma(r, q, -0x1p-1);                                            /* -1/2 */
-    const double l = fma(r * r, q, r);                                 /* ln(1 + r) */
-    return -fma((double)(ex - 32), 0x1.62e42fefa39efp-1, ln + l);
+    const uint32_t j = (bits >> 16) & 127u;
+    const float c = LOGTAB[2 * j], ln = LOGTAB[2 * j + 1];
+    const float r = fmaf(m, c, -1.0f);
+    float q = fmaf(r, -0.25f, 0x1.555556p-2f); /* -1/4, RN32(1/3) */
+    q = fmaf(r, q, -0.5f);
+    const float l = fmaf(r * r, q, r); /* ln(1 + r) */
+    const float kf = (float)k;
+    return -fmaf(kf, ECDNA_LN2_HI, fmaf(kf, ECDNA_LN2_LO, ln + l));
 }
+
+/* The channel's uniform ((w >> 9) + 0.5) 2^-23 (exact; below 1 - 2^-24, so u a0 < a0 and a zero-propensity last
+ * channel is never drawn). */
+static float chan_u(uint32_t w) { return fmaf((float)(w >> 9), 0x1p-23f, 0x1p-24f); }
 
 /* ------------------------------------------------------------ word stream */
 
@@ -530,17 +533,18 @@ static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16
             stop = ECDNA_STOP_MAX_TIME;
             break;
         }
-        /* propensities rate_i * population_i, population = update_state's vector */
-        double a[4];
-        a[0] = (double)rt.b0 * (double)nminus;
-        a[1] = (double)rt.b1 * (double)nplus;
-        a[2] = bd ? (double)rt.d0 * (double)nminus : 0.0;
-        a[3] = bd ? (double)rt.d1 * (double)nplus : 0.0;
-        double c0 = a[0];
-        double c1 = c0 + a[1];
-        double c2 = c1 + a[2];
-        double a0 = c2 + a[3];
-        if (!(a0 > 0.0)) {
+        /* propensities rate_i * population_i, population = update_state's vector; f32 (draw mapping v6) */
+        const float fnm = (float)nminus, fnp = (float)nplus;
+        float a[4];
+        a[0] = rt.b0 * fnm;
+        a[1] = rt.b1 * fnp;
+        a[2] = bd ? rt.d0 * fnm : 0.0f;
+        a[3] = bd ? rt.d1 * fnp : 0.0f;
+        float c0 = a[0];
+        float c1 = c0 + a[1];
+        float c2 = c1 + a[2];
+        float a0 = c2 + a[3];
+        if (!(a0 > 0.0f)) {
             stop = ECDNA_STOP_ABSORBING;
             break;
         }
@@ -556,9 +560,9 @@ static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16
         uint32_t w[4];
         event_block(p->seed, rid, e, w);
         /* direct method: channel by w1 against the cumulative propensities */
-        double target = (((double)w[1] + 0.5) * 0x1p-32) * a0;
+        float target = chan_u(w[1]) * a0;
         int ch = target < c0 ? 0 : (target < c1 ? 1 : (target < c2 ? 2 : 3));
-        double tau = oracle_softlog_neg(w[0]) / a0;
+        float tau = oracle_softlog_neg(w[0]) / a0; /* the correctly rounded f32 quotient */
         wstream ws;
         ws_init(&ws, p->seed, rid, e, w[2], w[3]);
         ws.sp[0] = spare[0];
@@ -607,9 +611,9 @@ static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16
         cnt[ch] += 1;
         e += 1;
         if (f32t)
-            t32 = t32 + (float)tau;
+            t32 = t32 + tau;
         else
-            t = t + tau; /* self.time += reaction.time (src/process.rs:184, 336) */
+            t = t + (double)tau; /* self.time += reaction.time (src/process.rs:184, 336); the f64 clock */
         if (hash_on) h = fnv_fold(h, x);
     }
     if (binned) {
@@ -708,7 +712,7 @@ static int validate(const ecdna_ssa_params_t* p, uint64_t row_stride, int want_r
     for (uint32_t s = 0; s < p->n_param_sets; ++s) { /* finite, non-negative rates */
         const float x[4] = {p->rates[s].b0, p->rates[s].b1, p->rates[s].d0, p->rates[s].d1};
         for (int i = 0; i < 4; ++i)
-            if (!(x[i] >= 0.f && x[i] <= FLT_MAX)) return ECDNA_E_INVALID;
+            if (!(x[i] == 0.f || (x[i] >= 0x1p-60f && x[i] <= 0x1p60f))) return ECDNA_E_INVALID;
     }
     if (p->process != ECDNA_PURE_BIRTH && p->process != ECDNA_BIRTH_DEATH) return ECDNA_E_INVALID;
     if (p->segregation < 0 || p->segregation > 3) return ECDNA_E_INVALID;

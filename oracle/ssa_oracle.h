@@ -32,8 +32,8 @@ extern "C" {
 
 /* ---- primitives (philox mode) ---- */
 void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
-/* -ln((w + 0.5) * 2^-32) by the engine's fixed-operation-order software log. */
-double oracle_softlog_neg(uint32_t w);
+/* -ln(((w >> 9) + 0.5) * 2^-23) by the engine's fixed-operation-order f32 software log (draw mapping v6). */
+float oracle_softlog_neg(uint32_t w);
 
 /* ---- whole runs ---- */
 /* Same contract as ecdna_ssa_run (include/ecdna_ssa.h) with host buffers; out_rows, if given,

@@ -121,8 +121,9 @@ def test_invalid_parameters_rejected(product_lib):
     s3 = abi.RunSpec(rates=((1, 1, 0, 0), (1, 2, 0, 0)), reps_per_set=2, n_replicates=8)
     bad.append(s3.params())  # replicate 7 -> set 3 >= 2 sets
     bad_rates = [abi.RunSpec(rates=(r,), n_replicates=4) for r in
-                 ((1, float("inf"), 0, 0), (1, 1, float("nan"), 0), (1, 1, 0, -0.5), (-1e-30, 1, 0, 0))]
-    bad += [r.params() for r in bad_rates]  # rates must be finite and >= 0
+                 ((1, float("inf"), 0, 0), (1, 1, float("nan"), 0), (1, 1, 0, -0.5), (-1e-30, 1, 0, 0),
+                  (1, 1e-20, 0, 0), (1, 1, 2e18, 0), (1e-45, 1, 0, 0))]
+    bad += [r.params() for r in bad_rates]  # rates must be 0 or in [2^-60, 2^60] (ABI v8)
     s4 = abi.RunSpec(n_replicates=4, flags=abi.FLAG_REFERENCE_DRAWS | abi.FLAG_BIN_STORE)
     bad.append(s4.params())  # the reference draws run the row store only
     keep = [s, s2, s3, s4, bad_rates]  # noqa: F841  (host arrays referenced by the params)
@@ -167,11 +168,12 @@ def test_set_cost_hint_in_params():
 
 
 def test_oracle_rejects_invalid_rates(oracle_mod):
-    """The oracle keeps the product's contract: rates finite and >= 0 (include/ecdna_ssa.h)."""
-    for r in ((1, float("inf"), 0, 0), (1, 1, float("nan"), 0), (1, 1, 0, -0.5)):
+    """The oracle keeps the product's contract: every rate 0 or in [2^-60, 2^60] (include/ecdna_ssa.h, ABI v8)."""
+    for r in ((1, float("inf"), 0, 0), (1, 1, float("nan"), 0), (1, 1, 0, -0.5), (1, 3.0e38, 0, 0),
+              (1, 1, 1e-45, 0), (2.0**60 * 1.01, 1, 0, 0)):
         with pytest.raises(ValueError):
             oracle_mod.run(abi.RunSpec(rates=(r,), n_replicates=2, max_cells=10))
-    oracle_mod.run(abi.RunSpec(rates=((0, 3.0e38, 0, 1e-45),), n_replicates=2, max_cells=10))
+    oracle_mod.run(abi.RunSpec(rates=((0, 2.0**60, 0, 2.0**-60),), n_replicates=2, max_cells=10))
 
 
 def test_runspec_rejects_values_ctypes_would_mask():

@@ -102,12 +102,13 @@ def test_c4_bench_whole_instance_bit_exact(engine_mod, oracle_mod):
 
 @pytest.mark.gpu
 def test_c3_bench_instance_bit_exact(engine_mod, oracle_mod):
-    """C3, the metric's line (2^20 replicates, K = 32 / u32, rotation): the occupancy-first schedule with rotation
-    on; replicates spread over the id range equal the oracle."""
+    """C3, the metric's line (2^20 replicates, K = 32 / u32, rotation): the max-ILP schedule (since draw mapping v6 it
+    keeps the occupancy-first build's four workgroups per CU) with rotation on; replicates spread over the id range
+    equal the oracle."""
     bench = _bench()
     spec = bench.workload_spec(0, 1 << 20, 1 << 20, workload="c3")
     ins, res = _run_with_instance(engine_mod, spec)
-    assert (ins["kernel"], ins["schedule"], ins["paired"], ins["bin_kmax"], ins["bin_c32"]) == (1, 0, 0, 32, 1), ins
-    assert ins["rotation"] == 1 and ins["runtime_flags"] == 0, ins
+    assert (ins["kernel"], ins["schedule"], ins["paired"], ins["bin_kmax"], ins["bin_c32"]) == (1, 1, 0, 32, 1), ins
+    assert ins["rotation"] == 1 and ins["runtime_flags"] == 0 and ins["blocks_per_cu"] == 4, ins
     for local in (0, 333_333, (1 << 20) - 256):
         _compare_sample(res, spec, oracle_mod, local, 256)

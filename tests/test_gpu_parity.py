@@ -162,11 +162,12 @@ def test_gpu_edge_sizes_match_oracle(flags, engine_mod, oracle_mod):
 @pytest.mark.gpu
 @pytest.mark.parametrize("flags", [H, H | abi.FLAG_BIN_STORE])
 def test_gpu_extreme_rates_match_oracle(flags, engine_mod, oracle_mod):
-    """Rates at the ends of the f32 range (a denormal 1e-45, 3e38) and mixtures of them: the time step
-    soft_log / a0 spans its whole range (the division without the compiler's range
-    handling must still equal the IEEE quotient), bit for bit against the oracle's C division."""
-    for i, rates in enumerate([(1e-45, 1e-45, 0.0, 1e-45), (3.0e38, 3.0e38, 1.0e38, 2.0e38),
-                               (1e-45, 3.0e38, 1e-45, 0.0), (2.5e-38, 1.5, 0.3, 7e-39)]):
+    """Rates at the ends of the allowed range (2^-60 and 2^60, ABI v8) and mixtures of them: the f32 time step
+    soft_log / a0 spans its whole range (the division without the compiler's range handling must
+    still equal the IEEE quotient), bit for bit against the oracle's C division."""
+    lo, hi = 2.0**-60, 2.0**60
+    for i, rates in enumerate([(lo, lo, 0.0, lo), (hi, hi, hi / 3, hi / 2), (lo, hi, lo, 0.0), (1.1 * lo, 1.5, 0.3, 7 * lo),
+                               (hi, 1e-12, 0.0, 3.3e11)]):
         spec = abi.RunSpec(seed=70 + i, process=abi.BIRTH_DEATH, rates=(rates,), n_replicates=300,
                            max_cells=400, init={1: 2, 40: 1}, max_time=float("inf"), flags=flags)
         _compare(engine_mod.run(spec, want_rows=True), oracle_mod.run(spec, mode="philox", want_rows=True),
