@@ -429,9 +429,11 @@ def main():
             "higher_is_better": True,
             "scaling": "weak" if weak else "strong",
             "vs_baseline": None,
-            "dtype": "u16+f32" if refdraws else "u16+f64",
+            # integer cell/counter work plus f32 propensities, channel and time step (draw mapping v6, the reference's
+            # own precision, src/main.rs:67, 139); the engine's clock accumulates in f64
+            "dtype": "u16+f32" if refdraws else "u16+f32 (f64 clock)",
             "draws": "reference (ChaCha8 seed*10+i, first-reaction, BINV/BTPE, f32 time; seed for seed)"
-                     if refdraws else "philox (the engine's draw mapping, DESIGN.md §3)",
+                     if refdraws else "philox (the engine's draw mapping v6, DESIGN.md §3)",
             "store": args.store,
             "data": "synthetic",
             "config": {
