@@ -1235,10 +1235,13 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
             // with target < c_i; the c_i are non-decreasing)
             // ((w1 >> 9) + 0.5) 2^-23 formed exactly by one fma (chan_u), times a0 (RN32)
             const float target = chan_u(w.y) * a0;
-            uint32_t ch = (target >= cA ? 1u : 0u);
-            if (BD) ch += (target >= cB ? 1u : 0u) + (target >= cC ? 1u : 0u);
-            const bool nplus_ev = (ch & 1u) != 0;  // ProliferateNPlus or DeathNPlus: a cell is picked
-            const bool prolif = ch == 1u;
+            // the channel as the three compares' lane masks (no integer channel on the event path; it is formed
+            // only for the event hash): ProliferateNMinus !gA, ProliferateNPlus gA & !gB, DeathNMinus gB & !gC,
+            // DeathNPlus gC
+            const bool gA = target >= cA, gB = BD && target >= cB, gC = BD && target >= cC;
+            const bool prolif = gA && !gB;
+            const bool death_nm = gB && !gC;
+            const bool nplus_ev = prolif || gC;  // ProliferateNPlus or DeathNPlus: a cell is picked
 
             CYC_MARK(9);
             WordStream ws;
@@ -1306,9 +1309,10 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                 const bool fast1 = ws.pos == 1 && n <= 32u;
                 const bool fast2 = ws.pos == 1 && n > 32u && n <= 64u && nsp >= 1u;
                 const bool fast = fast1 || fast2;
-                // branch-free: the low n bits of the 64-bit word (spare0 : w3), n clamped to 64
-                const uint64_t m64 = ~0ull >> (64u - min(n, 64u));
-                k1v = __popc(w.w & (uint32_t)m64) + __popc(sp0 & (uint32_t)(m64 >> 32));
+                // branch-free: the low n bits of the 64-bit word (spare0 : w3), moved to its top by one shift (the
+                // value only counts where fast: 1 <= n <= 64)
+                const uint64_t x64 = (((uint64_t)sp0 << 32) | w.w) << ((64u - n) & 63u);
+                k1v = __popc((uint32_t)(x64 >> 32)) + __popc((uint32_t)x64);
                 if (prolif && fast) ws.pos = fast1 ? 2u : 3u;
                 if (prolif && !fast && k <= 32767u) {  // larger copy numbers or a rejected pick: more words
                     PATH_STAT(5);
@@ -1397,16 +1401,17 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                 }
                 CYC_MARK(14);
                 spares_update(nplus_ev ? ws.pos : 0u, w.z, w.w, sp0, sp1, nsp);
-                nm = nm + ((ch == 0u || (prolif && un == 1u)) ? 1u : 0u) - ((BD && ch == 2u) ? 1u : 0u);
+                nm = nm + ((!gA || (prolif && un == 1u)) ? 1u : 0u) - (death_nm ? 1u : 0u);
                 n_un += (prolif && un != 0u) ? 1u : 0u;
-                if (BD) n_dm += ch == 2u ? 1u : 0u;
+                if (BD) n_dm += death_nm ? 1u : 0u;
                 e += 1;
                 if (f32t)
                     t32 = t32 + tau;
                 else
                     t = t + (double)tau;
                 if (hash_on) {
-                    const uint64_t x = (uint64_t)ch | (prolif ? ((uint64_t)k1v << 2) : 0ull) |
+                    const uint64_t ch = (uint64_t)gA + (uint64_t)gB + (uint64_t)gC;
+                    const uint64_t x = ch | (prolif ? ((uint64_t)k1v << 2) : 0ull) |
                                        (nplus_ev ? ((uint64_t)idx << 20) : 0ull);
                     h = (h ^ x) * kFnvPrime;
                 }
