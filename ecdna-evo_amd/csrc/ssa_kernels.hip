@@ -634,6 +634,11 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
     PATH_STATS_DECL;
     const uint32_t stop32 = a.stop_cells < 0xffffffffull ? (uint32_t)a.stop_cells : 0xffffffffu;
     const bool helper = PAIR && (threadIdx.x & 63u) >= 32u;  // PAIR: serves lane - 32, never owns a replicate
+    // the large-k row capacity, held in a VGPR for the event path's one compare (left to the compiler, the event
+    // loop's SGPR pressure had it reloaded from the kernel arguments in every iteration, with an lgkmcnt(0) wait
+    // that also drained the wave's outstanding LDS reads)
+    uint32_t big_cap_v = a.big_cap;
+    asm volatile("" : "+v"(big_cap_v));
 
     // packed counter add: bin b (0-based, copy number b + 1) / group g, by +d (d = +1, -1 or 0, as a
     // two's complement 32-bit word: a 16-bit field never borrows from its neighbour because it is >= 1
@@ -1102,13 +1107,14 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     const float cBA = cAA + pbf;
                     const float cCA = cBA + rd0 * fmA;
                     const float a0A = cCA + pdf;
-                    const uint32_t overA = f32t ? (uint32_t)(t32 >= a.max_time32) : (uint32_t)(t >= a.max_time);
+                    const bool overA = f32t ? (t32 >= a.max_time32) : (t >= a.max_time);
                     const float targetA = chan_u(wa.y) * a0A;
-                    const uint32_t chA = (uint32_t)(targetA >= cAA) + (uint32_t)(targetA >= cBA) +
-                                         (uint32_t)(targetA >= cCA);
-                    const uint32_t okA = (uint32_t)go & (uint32_t)(e < a.max_iter) & (uint32_t)(nm + npf < stop32) &
-                                         (overA ^ 1u) & (uint32_t)(a0A > 0.0f) & (~chA & 1u);
-                    const uint32_t nmB = nm + (uint32_t)(chA == 0u) - (uint32_t)(chA == 2u);
+                    // the channel as lane masks (ProliferateNMinus !g0, DeathNMinus g1 & !g2); conditions combined
+                    // with non-short-circuit & so that the step stays one basic block
+                    const bool g0A = targetA >= cAA, g1A = targetA >= cBA, g2A = targetA >= cCA;
+                    const bool dmA = g1A & !g2A;
+                    const bool cA = go & (e < a.max_iter) & (nm + npf < stop32) & !overA & (a0A > 0.0f) & (!g0A | dmA);
+                    const uint32_t nmB = nm + (g0A ? 0u : 1u) - (dmA ? 1u : 0u);
                     const float tauA = div_in_range(lga, a0A);
                     const double tB = t + (double)tauA;
                     const float t32B = t32 + tauA;
@@ -1118,30 +1124,31 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     const float cBB = cAB + pbf;
                     const float cCB = cBB + rd0 * fmB;
                     const float a0B = cCB + pdf;
-                    const uint32_t overB = f32t ? (uint32_t)(t32B >= a.max_time32) : (uint32_t)(tB >= a.max_time);
+                    const bool overB = f32t ? (t32B >= a.max_time32) : (tB >= a.max_time);
                     const float targetB = chan_u(y2) * a0B;
-                    const uint32_t chB = (uint32_t)(targetB >= cAB) + (uint32_t)(targetB >= cBB) +
-                                         (uint32_t)(targetB >= cCB);
-                    const uint32_t okB = okA & (uint32_t)pair_ok & (uint32_t)(e + 1u < a.max_iter) & (uint32_t)(nmB + npf < stop32) &
-                                         (overB ^ 1u) & (uint32_t)(a0B > 0.0f) & (~chB & 1u);
-                    const uint32_t nmC = nmB + (uint32_t)(chB == 0u) - (uint32_t)(chB == 2u);
+                    const bool g0B = targetB >= cAB, g1B = targetB >= cBB, g2B = targetB >= cCB;
+                    const bool dmB = g1B & !g2B;
+                    const bool cB = cA & pair_ok & (e + 1u < a.max_iter) & (nmB + npf < stop32) & !overB & (a0B > 0.0f) &
+                                    (!g0B | dmB);
+                    const uint32_t nmC = nmB + (g0B ? 0u : 1u) - (dmB ? 1u : 0u);
                     const float tauB = div_in_range(lg2, a0B);
                     // commit. An N- event consumes no stream word after w1, so its spare update pushes w2 and
                     // w3 onto the stack and leaves exactly those two (spares_update with used = 0).
-                    const bool cA = okA != 0u, cB = okB != 0u;
                     sp0 = cB ? w2 : (cA ? wa.w : sp0);
                     sp1 = cB ? z2 : (cA ? wa.z : sp1);
                     nsp = cA ? 2u : nsp;
                     nm = cB ? nmC : (cA ? nmB : nm);
-                    n_dm += (okA & (uint32_t)(chA == 2u)) + (okB & (uint32_t)(chB == 2u));
-                    e += okA + okB;
+                    n_dm += ((cA & dmA) ? 1u : 0u) + ((cB & dmB) ? 1u : 0u);
+                    e += (cA ? 1u : 0u) + (cB ? 1u : 0u);
                     if (f32t)
                         t32 = cB ? t32B + tauB : (cA ? t32B : t32);
                     else
                         t = cB ? tB + (double)tauB : (cA ? tB : t);
                     if (hash_on) {
-                        const uint64_t hA = (h ^ (uint64_t)chA) * kFnvPrime;
-                        const uint64_t hB = (hA ^ (uint64_t)chB) * kFnvPrime;
+                        const uint64_t chA = (uint64_t)g0A + (uint64_t)g1A + (uint64_t)g2A;
+                        const uint64_t chB = (uint64_t)g0B + (uint64_t)g1B + (uint64_t)g2B;
+                        const uint64_t hA = (h ^ chA) * kFnvPrime;
+                        const uint64_t hB = (hA ^ chB) * kFnvPrime;
                         h = cB ? hB : (cA ? hA : h);
                     }
                     go = cB;
@@ -1164,21 +1171,22 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                         } else {
                             const uint4 w2 = philox_event(e, pre, rk);
                             const float target2 = chan_u(w2.y) * a02;
-                            const uint32_t ch2 = (target2 >= cA2 ? 1u : 0u) + (target2 >= cB2 ? 1u : 0u) +
-                                                 (target2 >= cC2 ? 1u : 0u);
-                            if (ch2 & 1u) {
+                            // the channel as lane masks: ProliferateNMinus !g0, DeathNMinus g1 & !g2
+                            const bool g0 = target2 >= cA2, g1 = target2 >= cB2, g2 = target2 >= cC2;
+                            const bool dm = g1 & !g2;
+                            if (g0 & !dm) {  // an N+ event: the full event draws it
                                 go = false;
                             } else {
                                 const float tau2 = div_in_range(softlog_neg(w2.x, logtab), a02);
                                 spares_update(0u, w2.z, w2.w, sp0, sp1, nsp);
-                                nm = nm + (ch2 == 0u ? 1u : 0u) - (ch2 == 2u ? 1u : 0u);
-                                n_dm += ch2 == 2u ? 1u : 0u;
+                                nm = nm + (g0 ? 0u : 1u) - (dm ? 1u : 0u);
+                                n_dm += dm ? 1u : 0u;
                                 e += 1;
                                 if (f32t)
                                     t32 = t32 + tau2;
                                 else
                                     t = t + (double)tau2;
-                                if (hash_on) h = (h ^ (uint64_t)ch2) * kFnvPrime;
+                                if (hash_on) h = (h ^ ((uint64_t)g0 + (uint64_t)g1 + (uint64_t)g2)) * kFnvPrime;
                             }
                         }
                     }
@@ -1351,7 +1359,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
             // event the large-k row holds at most np + 1 cells, so neither can overflow while
             // np + 1 <= big_cap: one compare on the event path, the checks themselves in a rare block
             // (C3: 88.0 ms per launch without any big_cap check, 91.8 with it on every event, 89.3 gated).
-            if (np + 1u > a.big_cap) {
+            if (np + 1u > big_cap_v) {
                 PATH_STAT(7);
                 KArgs* const ra = rare_args();
                 if (prolif && ev_err == 0u && un == 0u && np + 1u > ra->cell_cap) ev_err = ECDNA_REP_ERR_CELL_CAP;
