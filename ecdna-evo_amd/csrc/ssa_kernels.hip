@@ -819,19 +819,16 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
 #ifdef ECDNA_ROT_STATS
     unsigned long long c_tick = 0, c_bound = 0, c_start = clock64();
 #endif
+    // PAIR: the loop is wave-uniform. A lane with nothing left to claim (and every helper, which owns no replicate)
+    // is `done` and idles under EXEC; the wave leaves when the ballot of lanes not done is empty, so a helper can
+    // never leave while its owner still runs (the owners' liveness is explicit, not read from EXEC). Without PAIR a
+    // lane leaves the loop as soon as it has nothing left (done stays false and folds away).
+    bool done = PAIR && helper;
     CYC_DECL;
     for (;;) {
         CYC_MARK(2);
         CYC_ADD(3, 1);
         ++ff_tick;
-        // PAIR: a helper leaves with the last owner of its wave (EXEC at the reconverged loop top holds the lanes
-        // still looping; owners are its low 32 bits). Read before the helper-only branch, whose EXEC would hide
-        // the owners (volatile: it is not sunk into the branch).
-        if (PAIR) {
-            uint64_t live;
-            asm volatile("s_mov_b64 %0, exec" : "=s"(live));
-            if (helper && (uint32_t)live == 0u) break;
-        }
         if (rot && ((++it & tick_mask) == 0u)) {  // ---- rotation tick (wave-uniform)
 #ifdef ECDNA_ROT_STATS
             const unsigned long long c0 = clock64();
@@ -873,7 +870,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
         const bool any_bound = __builtin_amdgcn_read_exec() & __ballot(!active);
 #endif
         // (a PAIR helper claims nothing: it skips the boundary and takes part in the fast-forward steps below)
-        if (!active && !(PAIR && helper)) {  // ---- replicate boundary (rare): write the finished one, pull the next
+        if (!active && !done) {  // ---- replicate boundary (rare): write the finished one, pull the next
             KArgs* const ra = rare_args();
             if (have) {
                 store_bag();
@@ -909,15 +906,24 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     kind = rot_claim(ra, (part + d) % kRotParts, true, i);
                     pinned = kind != 0u;
                 }
-                if (kind == 0u) break;
+                if (kind == 0u) {
+                    if (!PAIR) break;
+                    done = true;
+                }
+            } else if (young && __hip_atomic_load(ra->head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
+                                        ra->admit_remaining >= ra->n) {
+                if (!PAIR) break;
+                done = true;
             } else {
-                if (young &&
-                    __hip_atomic_load(ra->head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + ra->admit_remaining >= ra->n)
-                    break;
                 i = atomicAdd(ra->head, 1u);
-                if (i >= ra->n) break;
-                if (ra->order) i = ra->order[i];
+                if (i >= ra->n) {
+                    if (!PAIR) break;
+                    done = true;
+                } else if (ra->order) {
+                    i = ra->order[i];
+                }
             }
+            if (!done) {  // a replicate claimed
             have = true;
             active = true;
             li = i;
@@ -1020,7 +1026,9 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     active = false;
                 }
             }
+            }  // (a replicate claimed)
         }
+        if (PAIR && __builtin_amdgcn_ballot_w64(!done) == 0u) break;  // every lane of the wave done (wave-uniform)
 #ifdef ECDNA_ROT_STATS
         if (any_bound) c_bound += clock64() - cb0;
 #endif
