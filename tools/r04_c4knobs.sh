@@ -13,5 +13,6 @@ for rep in 1 2; do
   run PROBE_COST_HINT=0
   run ECDNA_SSA_SCHED=0
   run ECDNA_SSA_SCHED=0 ECDNA_SSA_BLOCKS_PER_CU=3
-  PROBE_KMAX=32 PROBE_FLAGS=0x20 timeout -k 10 200 python3 tools/probe_configs.py c4 | python3 -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print("K=32", round(d["stepper_ms"],1), "ms")"
+  run ECDNA_SSA_C32=1
+  run ECDNA_SSA_C32=1 ECDNA_SSA_SCHED=0
 done

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 4: parity of the working tree plus the latency-bound shapes and the C4 whole sweep for libraries A and B.
+set -euo pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+A=${A:-base}; B=${B:-u16}
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_random_parity.py tests/test_gpu_rotation.py \
+  tests/test_gpu_drain.py -q -x --timeout 300 --timeout-method thread > gpurun_out/ab_parity.log 2>&1 || { echo PARITY FAILED; tail -30 gpurun_out/ab_parity.log; exit 1; }
+tail -1 gpurun_out/ab_parity.log
+bash tools/ab_latency.sh $A $B 2>&1 | tail -24
+for rep in 1 2 3; do for n in $A $B; do
+  ECDNA_SSA_LIB=$PWD/ecdna-evo_amd/lib_ab/$n/libecdna_ssa.so PROBE_FLAGS=0x20 PROBE_KMAX=64 timeout -k 10 200 python3 tools/probe_configs.py c4 |
+    python3 -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print('$n c4 shard K64', round(d['stepper_ms'],1), 'ms')"
+done; done
+for rep in 1 2; do for n in $A $B; do
+  ECDNA_SSA_LIB=$PWD/ecdna-evo_amd/lib_ab/$n/libecdna_ssa.so PROBE_GPUS=1 PROBE_FLAGS=0x20 PROBE_KMAX=64 timeout -k 10 300 python3 tools/probe_configs.py c4 |
+    python3 -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print('$n c4 whole', round(d['stepper_ms'],1), 'ms')"
+done; done
