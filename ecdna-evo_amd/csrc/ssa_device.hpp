@@ -161,6 +161,26 @@ __device__ __forceinline__ float div_in_range(float n, float d) {
     return fmaf(fmaf(-d, q1, n), r1, q1);
 }
 
+// x << (s & 31) as one v_lshlrev_b32, which reads only the low five bits of its amount (C++ leaves a shift by
+// 32 or more undefined, so the compiler would keep an explicit mask)
+__device__ __forceinline__ uint32_t shl_lo5(uint32_t x, uint32_t s) {
+    uint32_t r;
+    asm("v_lshlrev_b32 %0, %1, %2" : "=v"(r) : "v"(s), "v"(x));
+    return r;
+}
+
+// (x & m) | y and (x << s) | y as one VALU each (the compiler splits them when it merges neighbouring ORs)
+__device__ __forceinline__ uint32_t and_or(uint32_t x, uint32_t m, uint32_t y) {
+    uint32_t r;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "i"(m), "v"(y));
+    return r;
+}
+__device__ __forceinline__ uint32_t lshl_or(uint32_t x, uint32_t s, uint32_t y) {
+    uint32_t r;
+    asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "i"(s), "v"(y));
+    return r;
+}
+
 // 32 x 32 -> 64-bit product as one v_mad_u64_u32 (the compiler widens a u32 * u64 into two)
 __device__ __forceinline__ uint64_t mul_u32_wide(uint32_t a, uint32_t b) {
     uint64_t d, carry;
