@@ -1,7 +1,8 @@
 """Loop-section cycle counters of the bin stepper over one launch (development tool): where a wave's time
 goes (replicate boundary, N- fast-forward, full event), per wave-iteration and per event. Needs a library
 built with -DECDNA_CYCLE_STATS (EXTRA=-DECDNA_CYCLE_STATS bash tools/ab_build.sh WORKTREE cyc), selected
-with ECDNA_SSA_LIB. Usage: [PROBE_KMAX=K] python tools/cycle_stats.py [c2|c3|c4|c5] (C4 and C5: the 8-GPU rank-0 shard)"""
+with ECDNA_SSA_LIB. Usage: [PROBE_KMAX=K] python tools/cycle_stats.py [c2|c3|c4|c5|c4k<ex>] (C4 and C5: the 8-GPU rank-0 shard; c4k<ex>:
+its sets of k0 = 2^ex)"""
 import ctypes as C
 import dataclasses
 import json
@@ -21,8 +22,11 @@ NAMES = ["cyc_boundary", "cyc_ff", "cyc_full", "iters", "ff_entries", "ff_steps"
 
 def main():
     name = sys.argv[1] if len(sys.argv) > 1 else "c5"
-    spec = probe_configs.CONFIGS[name](0, 8) if name in ("c4", "c5") else probe_configs.CONFIGS[name]()
-    kmax = int(os.environ.get("PROBE_KMAX", KMAX[name]))
+    if name.startswith("c4k"):  # c4k<ex>: the C4 shard's sets of k0 = 2^ex (probe_configs.c4_subset)
+        spec = probe_configs.c4_subset(int(name[3:]))
+    else:
+        spec = probe_configs.CONFIGS[name](0, 8) if name in ("c4", "c5") else probe_configs.CONFIGS[name]()
+    kmax = int(os.environ.get("PROBE_KMAX", KMAX.get(name, 64)))
     spec = dataclasses.replace(spec, flags=abi.FLAG_BIN_STORE, bin_kmax=kmax, _keep=[])
     lib = engine.lib()
     readers = []

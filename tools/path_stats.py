@@ -2,7 +2,7 @@
 C5 rank-0 shard of the 8-GPU layout (`c5`, K = 64). Needs a library built with -DECDNA_PATH_STATS
 (EXTRA=-DECDNA_PATH_STATS bash tools/ab_build.sh WORKTREE pstats), selected with ECDNA_SSA_LIB. Prints
 wave-iterations, active lanes, and per rare block the fraction of wave-iterations that execute it (at
-least one lane in the block). Usage: python tools/path_stats.py [c3|c5]"""
+least one lane in the block). Usage: python tools/path_stats.py [c3|c5|c4k<ex>]"""
 import ctypes as C
 import json
 import os
@@ -15,7 +15,12 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import probe_configs  # noqa: E402
 
 workload = sys.argv[1] if len(sys.argv) > 1 else "c3"
-if workload == "c5":
+if workload.startswith("c4k"):  # the C4 shard's sets of k0 = 2^ex (probe_configs.c4_subset), K = 64
+    import dataclasses
+
+    spec = dataclasses.replace(probe_configs.c4_subset(int(workload[3:])), flags=abi.FLAG_BIN_STORE,
+                               bin_kmax=int(os.environ.get("PROBE_KMAX", "64")), _keep=[])
+elif workload == "c5":
     import dataclasses
 
     spec = dataclasses.replace(probe_configs.c5_shard(0), flags=abi.FLAG_BIN_STORE, bin_kmax=64, _keep=[])

@@ -33,6 +33,21 @@ def c4_shard(rank=0, gpus=8, interleaved=None):
                        hist_bins=1025, flags=0, set_cost_hint=hint)
 
 
+def c4_subset(ex, gpus=8):
+    """The sets of one initial copy number k0 = 2^ex of the C4 sweep (128 sets), with the replicates per set one
+    rank of `gpus` holds: which sets set the 8-GPU shard's critical path (tools/c4_sub.py)."""
+    rates, inits = [], []
+    for i in range(ex * 128, ex * 128 + 128):
+        s = 1.0 + 1.5 * (i % 16) / 15.0
+        d = 0.7 * ((i // 16) % 8) / 7.0
+        rates.append((1.0, s, d, d))
+        inits.append({1 << ex: 1})
+    per = 4096 // gpus
+    return abi.RunSpec(seed=42, process=abi.BIRTH_DEATH, rates=rates, reps_per_set=per, n_replicates=128 * per,
+                       max_cells=10_000, init_per_set=inits, hist_bins=1025, flags=0,
+                       set_cost_hint=abi.cost_hint(rates, inits))
+
+
 def c5_shard(rank=0, gpus=8):
     n = 262_144 // gpus
     return abi.RunSpec(seed=42, process=abi.BIRTH_DEATH, rates=((1.0, 1.0, 0.9, 0.9),), reps_per_set=262_144,
