@@ -1293,12 +1293,35 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
             uint64_t m = mul_u32_wide(w.z, np);
             uint32_t idx, k;
             bool small;
+            // K = 64 / u32 in the max-ILP build (C5: the whole run and its 8-GPU shards): a large pick issues its row
+            // reads and its segregation's first Philox block ahead of the bin search, so that the wave waits on the
+            // row's memory latency behind that work: the picked cell's copy number, the row's tail (what swap_remove
+            // moves when the picked cell leaves the row: nb is unchanged up to there) and, for a proliferation,
+            // block 1 of the stream (a copy number above 64 needs more than w3 and the two spares: binomial_half's
+            // first block is block 1). The same words and values as the loads and blocks they replace. (C5 whole
+            // 29.3 -> 28.8 s; with u16 counters, the C4 shard, whose waves share their SIMD until the drain, lost
+            // 5 %: profiles/r04p_large_pick_ahead_ab.txt)
+            constexpr bool kAhead = SCH == 1 && NG == 8 && C32;
+            uint32_t k_ahead = 0, tail_ahead = 0;
+            bool ahead = false;
             if (SCH == 1) {
                 // the max-ILP build (lone waves): one branch for both rare cases. The bins are searched with the
                 // first word's index, and a lane whose Lemire test may reject redoes the pick inside the branch,
                 // after its rejection loop (C2 8.1 -> 7.5 ms; the occupancy build keeps two branches: C3 +0.8 %)
                 idx = (uint32_t)(m >> 32);
                 small = idx < ns;
+                const uint32_t idx0 = idx;
+                if (kAhead) {
+                    ahead = nplus_ev & !small;
+                    if (ahead) {
+                        k_ahead = gload_u16_l2(row + (idx - ns));
+                        tail_ahead = gload_u16_l2(row + (nb - 1u));
+                        if (prolif) {
+                            ws.blk = philox4x32_10(make_uint4(e, 1u, rid_lo, rid_hi), rk);
+                            ws.blk_id = 1u;
+                        }
+                    }
+                }
                 k = bin_find(small ? idx : 0u);
                 if (nplus_ev & (((uint32_t)m < np) | !small)) {  // Lemire rejection or the large-k row (rare)
                     if ((uint32_t)m < np) {
@@ -1311,7 +1334,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     }
                     if (!small) {
                         PATH_STAT(4);
-                        k = gload_u16_l2(row + (idx - ns));
+                        k = (kAhead && ahead && idx == idx0) ? k_ahead : gload_u16_l2(row + (idx - ns));
                     }
                 }
             } else {
@@ -1426,7 +1449,8 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                         }
                     }
                     if (open != 0xffffffffu) {  // swap_remove(open) from B
-                        if (open != nb - 1) row[open] = (uint16_t)gload_u16_l2(row + nb - 1);
+                        if (open != nb - 1)
+                            row[open] = (uint16_t)((kAhead && ahead) ? tail_ahead : gload_u16_l2(row + nb - 1));
                         nb -= 1;
                     }
                 }
