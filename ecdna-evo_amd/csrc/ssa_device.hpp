@@ -251,8 +251,10 @@ struct WordStream {
         while (n) {
             const uint32_t q = pos - 2u - nsp;  // stream offset inside the block region
             const uint32_t j = (q >> 2) + 1u;
-            blk = block(make_uint4(e, j, rid_lo, rid_hi));
-            blk_id = j;
+            if (j != blk_id) {  // (the stepper may have formed block 1 ahead, or the Lemire loop this block)
+                blk = block(make_uint4(e, j, rid_lo, rid_hi));
+                blk_id = j;
+            }
             const uint32_t t0 = q & 3u;
             const uint32_t w[4] = {blk.x, blk.y, blk.z, blk.w};
 #pragma unroll
