@@ -89,16 +89,27 @@ BENCH_BIN_KMAX = 32
 # faster than 64; C2), K = 64 where copy numbers spread (C4: k0 up to 128, 8-GPU makespan 156 -> 131 ms;
 # C5: 1e6 cells)
 WORKLOAD_KMAX = {"c2": 32, "c3": BENCH_BIN_KMAX, "c4": 64, "c5": 64}
+# C5 holding more replicates on a GPU than K = 64's grid has lanes (131,072: two workgroups per CU, LDS-bound): K = 32
+# (four workgroups per CU, one replicate per lane for the whole run on one GPU: 22.6 against 28.8 s); its 8-GPU shards
+# (32,768 replicates, paired lanes) stay at K = 64 (9.9 against 10.9 s), profiles/r04s_c5_kmax.txt
+C5_K32_ABOVE = 131_072
+
+
+def default_kmax(workload: str, n: int) -> int:
+    """The workload's bin store K for a GPU holding n replicates."""
+    if workload == "c5" and n > C5_K32_ABOVE:
+        return 32
+    return WORKLOAD_KMAX[workload]
 
 
 def workload_spec(first: int, n: int, total: int, seed: int = 42, device: int = 0, store: str = "bins",
                   bin_kmax: Optional[int] = None, workload: str = "c3", stride: int = 1,
                   max_cells: Optional[int] = None) -> abi.RunSpec:
     """Replicates first, first + stride, ... (n of them) of the workload's `total` (SURVEY.md §8d shapes);
-    bin_kmax None = the workload's default (WORKLOAD_KMAX); max_cells None = the workload's (rehearsals of
+    bin_kmax None = the workload's default for n replicates (default_kmax); max_cells None = the workload's (rehearsals of
     the multi-rank paths shrink it, tests/test_gpu_bench_dist.py)."""
     if bin_kmax is None:
-        bin_kmax = WORKLOAD_KMAX[workload]
+        bin_kmax = default_kmax(workload, n)
     common = dict(seed=seed, first_replicate=first, n_replicates=n, replicate_stride=stride, hist_bins=1025,
                   flags=abi.FLAG_BIN_STORE if store == "bins" else 0, device=device)
     if workload == "c3":

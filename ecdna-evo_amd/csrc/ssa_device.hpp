@@ -238,7 +238,9 @@ struct WordStream {
     // words popcounted branch-free. (Word by word, next() generates a block whenever ANY lane of the
     // wave crosses a block boundary, and lanes sit at different stream offsets: large copy numbers then
     // ran a Philox block for almost every word.) block(c): Philox4x32-10 of counter c under the run's key.
-    template <class Block>
+    // kReuse: keep a block already in `blk` (the stepper's K = 64 / u32 max-ILP instances form block 1 ahead);
+    // elsewhere every block is formed here, as before (no compare on their path)
+    template <bool kReuse, class Block>
     __device__ __forceinline__ uint32_t binomial_half_with(uint32_t n, const Block& block) {
         uint32_t c = 0;
         while (n && pos < 2u + nsp) {  // w3 and the spares (at most three words; no Philox block here)
@@ -251,7 +253,7 @@ struct WordStream {
         while (n) {
             const uint32_t q = pos - 2u - nsp;  // stream offset inside the block region
             const uint32_t j = (q >> 2) + 1u;
-            if (j != blk_id) {  // (the stepper may have formed block 1 ahead, or the Lemire loop this block)
+            if (!kReuse || j != blk_id) {  // (kReuse: block 1 formed ahead, or this block by the Lemire loop)
                 blk = block(make_uint4(e, j, rid_lo, rid_hi));
                 blk_id = j;
             }
@@ -322,14 +324,15 @@ struct WordStream {
 
     // with the key schedule formed per block (k0, k1)
     __device__ __forceinline__ uint32_t binomial_half(uint32_t n) {
-        return binomial_half_with(n, [&](uint4 c4) { return philox4x32_10(c4, k0, k1); });
+        return binomial_half_with<false>(n, [&](uint4 c4) { return philox4x32_10(c4, k0, k1); });
     }
 
     // with the kernel's VGPR round keys. (A reference, never a nullable pointer: a null test of the keys'
     // private-memory address does not fold on AMDGPU, where private null is not address 0, and the test alone
     // kept the 20 keys in scratch, reloaded at every Philox round of every kernel that had it.)
+    template <bool kReuse = false>
     __device__ __forceinline__ uint32_t binomial_half(uint32_t n, const PhiloxKeys& rk) {
-        return binomial_half_with(n, [&](uint4 c4) { return philox4x32_10(c4, rk); });
+        return binomial_half_with<kReuse>(n, [&](uint4 c4) { return philox4x32_10(c4, rk); });
     }
 };
 

@@ -1370,7 +1370,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                 if (prolif && fast) ws.pos = fast1 ? 2u : 3u;
                 if (prolif && !fast && k <= 32767u) {  // larger copy numbers or a rejected pick: more words
                     PATH_STAT(5);
-                    k1v = ws.binomial_half(n, rk);
+                    k1v = ws.binomial_half<kAhead>(n, rk);
                 }
                 if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN && prolif && (k1v == 0u || k1v == n)) {
                     // src/segregation.rs:157-174: redraw while uneven (the first draw above was try 1)
@@ -1385,7 +1385,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                                 ev_err = ECDNA_REP_ERR_REJECTION;
                                 break;
                             }
-                            k1v = ws.binomial_half(n, rk);
+                            k1v = ws.binomial_half<kAhead>(n, rk);
                             ++tries;
                         }
                     }

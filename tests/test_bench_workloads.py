@@ -63,3 +63,13 @@ def test_workload_bin_kmax_defaults(workload, kmax):
     assert bench.workload_spec(0, 8, total, workload=workload).bin_kmax == kmax
     assert bench.workload_spec(0, 8, total, workload=workload, bin_kmax=256).bin_kmax == 256
     assert bench.workload_spec(0, 8, total, workload=workload, store="rows").bin_kmax == 0
+
+
+def test_c5_bin_kmax_by_replicates_per_gpu():
+    """C5 takes K = 32 where a GPU holds more replicates than K = 64's grid has lanes (the whole run on one GPU), and
+    K = 64 for the 8-, 4- and 2-GPU shards (profiles/r04s_c5_kmax.txt)."""
+    total = bench.WORKLOADS["c5"][0]
+    assert bench.workload_spec(0, total, total, workload="c5").bin_kmax == 32
+    for gpus in (2, 4, 8):
+        assert bench.workload_spec(0, total // gpus, total, workload="c5").bin_kmax == 64
+    assert bench.workload_spec(0, total, total, workload="c5", bin_kmax=64).bin_kmax == 64

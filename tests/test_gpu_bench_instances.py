@@ -101,6 +101,23 @@ def test_c4_bench_whole_instance_bit_exact(engine_mod, oracle_mod):
 
 
 @pytest.mark.gpu
+def test_c5_bench_whole_instance_bit_exact(engine_mod, oracle_mod):
+    """C5 on one GPU as `bench.py --workload c5` runs it (262,144 replicates, K = 32 with u32 counters since r04s:
+    four workgroups per CU, one replicate per lane; large-k row 2^16): the max-ILP schedule, unpaired; replicates
+    0..3 and two from the end (about 2e7 events each, to 1e6 cells) equal the oracle."""
+    bench = _bench()
+    spec = bench.workload_spec(0, 262_144, 262_144, workload="c5")
+    assert spec.flags == abi.FLAG_BIN_STORE and spec.bin_kmax == 32 and spec.big_cap == 1 << 16
+    ins, res = _run_with_instance(engine_mod, spec)
+    assert (ins["kernel"], ins["schedule"], ins["paired"], ins["bin_kmax"], ins["bin_c32"]) == (1, 1, 0, 32, 1), ins
+    assert ins["blocks_per_cu"] == 4 and ins["runtime_flags"] == 0, ins
+    s = res.summaries
+    assert np.all(s["error"] == 0) and np.all(s["stop_reason"] == abi.STOP_MAX_CELLS)
+    _compare_sample(res, spec, oracle_mod, 0, 4, threads=4)
+    _compare_sample(res, spec, oracle_mod, 262_142, 2, threads=2)
+
+
+@pytest.mark.gpu
 def test_c3_bench_instance_bit_exact(engine_mod, oracle_mod):
     """C3, the metric's line (2^20 replicates, K = 32 / u32, rotation): the max-ILP schedule (since draw mapping v6 it
     keeps the occupancy-first build's four workgroups per CU) with rotation on; replicates spread over the id range
