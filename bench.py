@@ -15,6 +15,10 @@ Cell store (--store): "bins" (default, ECDNA_FLAG_BIN_STORE: per-replicate copy-
 LDS) or "rows" (one u16 per cell in HBM in the reference's swap_remove order). Both
 simulate the same process and count the same events; each is bit-exact with its oracle restatement.
 
+`--scaling strong` is the metric's fixed-total reading of C3: 2^20 replicates in total, rank g of N runs the
+contiguous ids [g 2^20 / N, (g+1) 2^20 / N) — the reference's fixed `runs` replicates over its worker pool
+(src/main.rs:212-224). At N=1 it is the same run as the weak line.
+
 Other BASELINE.json configs (--workload; the default line above is C3): c2 = 65,536 pure-birth replicates
 to 1e4 cells (configs[1]); c4 = the ABC sweep, 1024 (b1, d, k0) parameter sets x 4,096 replicates
 (configs[3]); c5 = 262,144 birth-death turnover replicates from 1,000 cells to 1e6 cells or t = 1000
@@ -279,6 +283,10 @@ def main():
     ap.add_argument("--dump-hist", default="", help="rank 0 saves the reduced histogram and totals (.npz)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3",
                     help="BASELINE.json config; c3 (default) is the metric's weak-scaling line")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="c3 only: weak (default) = 2^20 replicates per GPU; strong = 2^20 replicates in total, "
+                         "contiguous shards of 2^20 / N (the reference's fixed `runs` over its worker pool, "
+                         "src/main.rs:212-224)")
     ap.add_argument("--total", type=int, default=None,
                     help="rehearsal only: replicates in total for the strong-scaling workloads (c2/c4/c5)")
     ap.add_argument("--max-cells", type=int, default=None, help="rehearsal only: override the workload's cell cap")
@@ -306,12 +314,20 @@ def main():
     else:
         torch.cuda.set_device(0)
     n_gpus = world
-    weak = args.workload == "c3"
+    if args.scaling == "strong" and args.workload != "c3":
+        ap.error("--scaling strong applies to c3 (the other workloads are fixed totals already)")
+    weak = args.workload == "c3" and args.scaling == "weak"
+    c3_strong = args.workload == "c3" and args.scaling == "strong"
     if weak:  # the metric's line: 2^20 replicates per GPU, rank g owns ids [g 2^20, (g+1) 2^20)
         reps = args.reps_per_gpu
         total = reps * n_gpus
         first, n = shard.weak_range(rank, reps)
         stride = 1
+    elif c3_strong:  # the metric's fixed-total reading: 2^20 in total, rank g owns a contiguous 1/N of them
+        total = args.total or REPS_PER_GPU
+        first, n = shard.shard_range(rank, n_gpus, total)
+        stride = 1
+        reps = n
     else:  # a fixed total over the ranks, interleaved ids
         total = args.total or WORKLOADS[args.workload][0]
         first, n, stride = shard.interleaved_range(rank, n_gpus, total)
@@ -388,7 +404,8 @@ def main():
     if rank == 0:
         avg_kernel_s = sum(kernel_ms) / len(kernel_ms) * 1e-3
         achieved = local_alg / avg_kernel_s / 1e9
-        pmc = load_pmc(args.store) if weak and not refdraws else {}  # (the committed PMC summaries: C3, philox)
+        # (the committed PMC summaries: C3, philox; the strong reading's one-GPU run is the same launch)
+        pmc = load_pmc(args.store) if args.workload == "c3" and n_gpus == 1 and not refdraws else {}
         traffic = pmc.get("hbm_bytes_per_launch")
         kernel_eps = local_events / avg_kernel_s
         transactions = None
@@ -430,7 +447,7 @@ def main():
         chunk, lanes = ctx.geometry()
         instance = ctx.instance()  # the kernel instance timed (auto rules of ecdna_ssa_ctx_create, ABI v7)
         line = {
-            "metric": METRIC if weak else f"Gillespie reaction-events/sec, {args.workload.upper()}",
+            "metric": METRIC if args.workload == "c3" else f"Gillespie reaction-events/sec, {args.workload.upper()}",
             "value": events_per_step * args.steps / elapsed,
             "unit": "events/s",
             "n_gpus": n_gpus,
@@ -448,7 +465,9 @@ def main():
             "store": args.store,
             "data": "synthetic",
             "config": {
-                "workload": WORKLOADS[args.workload][1],
+                "workload": WORKLOADS[args.workload][1] if not c3_strong else
+                            "C3 (BASELINE.json configs[2]), fixed total: 2^20 replicates over all GPUs, birth-death b0=1 "
+                            "b1=1.5 d0=d1=0.3, binomial segregation, init {1:1}, stop 1e4 cells or t=17, seed 42",
                 "cell_store": f"bins (copy-number counters in LDS, k<={spec.bin_kmax}; ECDNA_FLAG_BIN_STORE)"
                               if args.store == "bins" else "rows (u16 per cell in HBM, swap_remove order)",
                 "replicates_per_gpu": reps,
@@ -456,7 +475,7 @@ def main():
                 "events_per_step": events_per_step,
                 "stop_reasons": stop_reasons,
                 "replicate_errors": errors,
-                "parallelism": f"replicas{n_gpus} ({'contiguous' if weak else 'interleaved'} replicate-id shards, "
+                "parallelism": f"replicas{n_gpus} ({'contiguous' if args.workload == 'c3' else 'interleaved'} replicate-id shards, "
                                f"1 RCCL all-reduce of the histogram)",
                 "grid_lanes": lanes,
                 "instance": instance,

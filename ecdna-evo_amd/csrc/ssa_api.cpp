@@ -843,10 +843,14 @@ int ecdna_ssa_ctx_instance(const ecdna_ssa_ctx* c, ecdna_ssa_instance_t* out) {
     r.cost_order = c->d_order ? 1 : 0;
     r.block_lanes = c->stepper_block;
     r.cus = (uint32_t)c->cus;
-    r.blocks_per_cu = c->cus ? c->stepper_blocks_cap / (uint32_t)c->cus : 0u;
+    // the grid actually launched (the largest chunk's; a small or paired run launches fewer blocks than the
+    // occupancy cap), and its workgroups per CU rounded up
+    uint32_t launched = 0;
+    for (const auto& ch : c->chunks) launched = std::max<uint32_t>(launched, ch.blocks);
+    r.blocks_per_cu = c->cus ? (launched + (uint32_t)c->cus - 1u) / (uint32_t)c->cus : 0u;
     r.n_chunks = (uint32_t)c->chunks.size();
     r.chunk_replicates = c->chunk_reps;
-    r.grid_lanes = (uint64_t)c->stepper_blocks_cap * c->stepper_block;
+    r.grid_lanes = (uint64_t)launched * c->stepper_block;
     hipFuncAttributes fa{};
     if (fn && hipFuncGetAttributes(&fa, fn) == hipSuccess) {
         r.vgprs = (uint32_t)fa.numRegs;

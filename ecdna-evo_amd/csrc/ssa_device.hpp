@@ -2,8 +2,8 @@
 //
 // The draw mapping is the engine's own definition; the CPU
 // oracle (oracle/ssa_oracle.c) restates it independently and the parity tests
-// require bit-identical results. Every f64 operation here is a correctly
-// rounded IEEE add/sub/mul/div in a fixed order; the file is compiled with
+// require bit-identical results. Every f32 / f64 operation here is a correctly
+// rounded IEEE add/sub/mul/div/fma in a fixed order; the file is compiled with
 // -ffp-contract=off and additionally pins contraction off below, so no FMA
 // fusion can change a rounding.
 #pragma once
@@ -142,9 +142,12 @@ __device__ __forceinline__ float softlog_end(const SoftlogParts& p) {
 
 __device__ __forceinline__ float softlog_neg(uint32_t w, const float2* tab) { return softlog_end(softlog_begin(w, tab)); }
 
-// The channel's uniform, draw mapping v6: ((w >> 9) + 0.5) 2^-23, formed exactly by one fma. Below 1 - 2^-24, so
-// target = u a0 (RN32) stays below a0 and a last channel of zero propensity is never drawn.
-__device__ __forceinline__ float chan_u(uint32_t w) { return fmaf((float)(w >> 9), 0x1p-23f, 0x1p-24f); }
+// The channel's target, draw mapping v7: u = (w + 0.5) 2^-32 from all 32 bits of w1, exact in f64 (one
+// fma: w + 0.5 has 33 significant bits), times the f64 total propensity A (RN64). u <= 1 - 2^-33, so the target stays
+// below A and a last channel of zero propensity is never drawn; u >= 2^-33 and A >= 2^-60 keep it above 0, so a first
+// channel of zero propensity is never drawn either. (v6 took 23 bits of w1 and f32 cumulative sums: a channel below
+// ~2^-24 of the total could not fire)
+__device__ __forceinline__ double chan_target(uint32_t w, double a) { return fma((double)w, 0x1p-32, 0x1p-33) * a; }
 
 // n / d, the correctly rounded IEEE f32 quotient (the oracle's C division), for operands in the stepper's range.
 // LLVM lowers an f32 divide to v_div_scale x2, v_rcp_f32, the Newton step, the quotient and two residual

@@ -190,15 +190,17 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
             }
         }
 
-        // propensities rate_i * population_i over [n-, n+(, n-, n+)], f32 (draw mapping v6)
+        // propensities rate_i * population_i over [n-, n+(, n-, n+)] in f32 (the reference's own, src/main.rs:67, 139),
+        // their cumulative sums in f64 (draw mapping v7); the time step divides by a0 = RN32(A)
         const float fnm = (float)nm, fnp = (float)np;
-        const float cA = b0 * fnm;
-        const float cB = cA + b1 * fnp;
-        float cC = cB, a0 = cB;
+        const double cA = (double)(b0 * fnm);
+        const double cB = cA + (double)(b1 * fnp);
+        double cC = cB, A = cB;
         if (BD) {
-            cC = cB + d0 * fnm;
-            a0 = cC + d1 * fnp;
+            cC = cB + (double)(d0 * fnm);
+            A = cC + (double)(d1 * fnp);
         }
+        const float a0 = (float)A;
 
         // stop checks, in the order of DESIGN.md §3.1 (selects, last write = first check)
         {
@@ -247,7 +249,7 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
 
         const uint32_t rid_lo = (uint32_t)rid, rid_hi = (uint32_t)(rid >> 32);
         const uint4 w = philox4x32_10(make_uint4(e, 0u, rid_lo, rid_hi), k0, k1);
-        const float target = chan_u(w.y) * a0;
+        const double target = chan_target(w.y, A);
         uint32_t ch;
         if (BD)
             ch = target < cA ? 0u : (target < cB ? 1u : (target < cC ? 2u : 3u));
@@ -1059,9 +1061,9 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
         if (BD && kFfMax && !a.n_snap && (ff_mode || (ff_tick & (ECDNA_FF_TEST_EVERY - 1u)) == 0u)) {
             const uint32_t npf = ns + nb;  // n+ is fixed during N- events
             const float fpf = (float)npf;
-            const float pbf = rb1 * fpf, pdf = rd1 * fpf;
+            const double pbf = (double)(rb1 * fpf), pdf = (double)(rd1 * fpf);
             const float pm = rb0 * (float)nm + rd0 * (float)nm;
-            const bool heavy = active && pm * 8.0f >= (pm + pbf + pdf) * (float)ECDNA_FF_ENTER8;  // (speed only)
+            const bool heavy = active && pm * 8.0f >= (pm + (float)pbf + (float)pdf) * (float)ECDNA_FF_ENTER8;  // (speed only)
             const uint32_t n_in = (uint32_t)__builtin_popcountll(__ballot(active));
             ff_mode = n_in != 0u && (uint32_t)__builtin_popcountll(__ballot(heavy)) * 8u >= n_in * ECDNA_FF_ENTER8;
             CYC_ADD(4, ff_mode ? 1u : 0u);
@@ -1126,12 +1128,13 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     // event e (conditions as 0/1 words combined with bitwise ops: no short-circuit branches, so
                     // the step stays one basic block for the scheduler)
                     const float fmA = (float)nm;
-                    const float cAA = rb0 * fmA;
-                    const float cBA = cAA + pbf;
-                    const float cCA = cBA + rd0 * fmA;
-                    const float a0A = cCA + pdf;
+                    const double cAA = (double)(rb0 * fmA);
+                    const double cBA = cAA + pbf;
+                    const double cCA = cBA + (double)(rd0 * fmA);
+                    const double AA = cCA + pdf;
+                    const float a0A = (float)AA;
                     const bool overA = f32t ? (t32 >= a.max_time32) : (t >= a.max_time);
-                    const float targetA = chan_u(wa.y) * a0A;
+                    const double targetA = chan_target(wa.y, AA);
                     // the channel as lane masks (ProliferateNMinus !g0, DeathNMinus g1 & !g2); conditions combined
                     // with non-short-circuit & so that the step stays one basic block
                     const bool g0A = targetA >= cAA, g1A = targetA >= cBA, g2A = targetA >= cCA;
@@ -1143,12 +1146,13 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     const float t32B = t32 + tauA;
                     // event e + 1, from the state after e
                     const float fmB = (float)nmB;
-                    const float cAB = rb0 * fmB;
-                    const float cBB = cAB + pbf;
-                    const float cCB = cBB + rd0 * fmB;
-                    const float a0B = cCB + pdf;
+                    const double cAB = (double)(rb0 * fmB);
+                    const double cBB = cAB + pbf;
+                    const double cCB = cBB + (double)(rd0 * fmB);
+                    const double AB = cCB + pdf;
+                    const float a0B = (float)AB;
                     const bool overB = f32t ? (t32B >= a.max_time32) : (tB >= a.max_time);
-                    const float targetB = chan_u(y2) * a0B;
+                    const double targetB = chan_target(y2, AB);
                     const bool g0B = targetB >= cAB, g1B = targetB >= cBB, g2B = targetB >= cCB;
                     const bool dmB = g1B & !g2B;
                     const bool cB = cA & pair_ok & (e + 1u < a.max_iter) & (nmB + npf < stop32) & !overB & (a0B > 0.0f) &
@@ -1184,16 +1188,17 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     CYC_ADD(5, 1);
                     if (go) {
                         const float fm2 = (float)nm;
-                        const float cA2 = rb0 * fm2;
-                        const float cB2 = cA2 + pbf;
-                        const float cC2 = cB2 + rd0 * fm2;
-                        const float a02 = cC2 + pdf;
+                        const double cA2 = (double)(rb0 * fm2);
+                        const double cB2 = cA2 + pbf;
+                        const double cC2 = cB2 + (double)(rd0 * fm2);
+                        const double A2 = cC2 + pdf;
+                        const float a02 = (float)A2;
                         const bool t_over2 = f32t ? (t32 >= a.max_time32) : (t >= a.max_time);
                         if ((e >= a.max_iter) || nm + npf >= stop32 || t_over2 || !(a02 > 0.0f)) {
                             go = false;
                         } else {
                             const uint4 w2 = philox_event(e, pre, rk);
-                            const float target2 = chan_u(w2.y) * a02;
+                            const double target2 = chan_target(w2.y, A2);
                             // the channel as lane masks: ProliferateNMinus !g0, DeathNMinus g1 & !g2
                             const bool g0 = target2 >= cA2, g1 = target2 >= cB2, g2 = target2 >= cC2;
                             const bool dm = g1 & !g2;
@@ -1223,15 +1228,17 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
         PATH_STAT_LANES(1);
         const uint32_t np = ns + nb;
 
-        // propensities rate_i * population_i over [n-, n+(, n-, n+)], f32 (draw mapping v6)
+        // propensities rate_i * population_i over [n-, n+(, n-, n+)] in f32 (the reference's own, src/main.rs:67, 139),
+        // their cumulative sums in f64 (draw mapping v7); the time step divides by a0 = RN32(A)
         const float fm = (float)nm, fp = (float)np;
-        const float cA = rb0 * fm;
-        const float cB = cA + rb1 * fp;
-        float cC = cB, a0 = cB;
+        const double cA = (double)(rb0 * fm);
+        const double cB = cA + (double)(rb1 * fp);
+        double cC = cB, A = cB;
         if (BD) {
-            cC = cB + rd0 * fm;
-            a0 = cC + rd1 * fp;
+            cC = cB + (double)(rd0 * fm);
+            A = cC + (double)(rd1 * fp);
         }
+        const float a0 = (float)A;
         // stop checks: one test here, the reason only when a lane stops
         const bool t_over = f32t ? (t32 >= a.max_time32) : (t >= a.max_time);
         const bool cells_over = nm + np >= stop32;  // (u32: cell counts stay below 2^32)
@@ -1263,9 +1270,8 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
             const uint32_t rid_lo = (uint32_t)rid, rid_hi = (uint32_t)(rid >> 32);
             const uint4 w = philox_event(e, pre, rk);
             // direct method: the channel is the number of cumulative propensities <= target (the first i
-            // with target < c_i; the c_i are non-decreasing)
-            // ((w1 >> 9) + 0.5) 2^-23 formed exactly by one fma (chan_u), times a0 (RN32)
-            const float target = chan_u(w.y) * a0;
+            // with target < c_i; the c_i are non-decreasing); (w1 + 0.5) 2^-32 times A, in f64 (chan_target)
+            const double target = chan_target(w.y, A);
             // the channel as the three compares' lane masks (no integer channel on the event path; it is formed
             // only for the event hash): ProliferateNMinus !gA, ProliferateNPlus gA & !gB, DeathNMinus gB & !gC,
             // DeathNPlus gC

@@ -14,7 +14,7 @@ from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 # ecdna_process_t (ProcessType, src/clap_app.rs:311-315)
 PURE_BIRTH = 0

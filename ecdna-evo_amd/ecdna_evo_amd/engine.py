@@ -121,7 +121,10 @@ def lib():
     L.ecdna_ssa_reduce_hist.restype = C.c_int
     L.ecdna_ssa_ctx_reduce.argtypes = [C.c_void_p, C.c_void_p]
     L.ecdna_ssa_ctx_reduce.restype = C.c_int
-    if L.ecdna_ssa_abi_version() != abi.ABI_VERSION:
+    ver = L.ecdna_ssa_abi_version()
+    # (a same-box A/B, tools/ab_build.sh, may load a library of an earlier ABI version whose layout is unchanged:
+    # ECDNA_SSA_ABI_ANY=1 accepts it from 8 on; results then follow that library's draw mapping)
+    if ver != abi.ABI_VERSION and not (os.environ.get("ECDNA_SSA_ABI_ANY") == "1" and ver >= 8):
         raise EngineError("ABI version mismatch between libecdna_ssa.so and ecdna_evo_amd.abi")
     _lib = L
     return L

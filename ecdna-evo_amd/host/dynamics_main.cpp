@@ -256,6 +256,14 @@ Options parse(int argc, char** argv) {
     if (o.reference_draws && ((o.has_cell_store && !o.rows) || o.has_bin_kmax))
         usage_error("the argument '--draws reference' cannot be used with '--cell-store bins' or '--bin-kmax'");
     if (o.reference_draws) o.rows = true;
+    // The engine's rate range (include/ecdna_ssa.h, since ABI v8): 0 or [2^-60, 2^60]; a divergence from the
+    // reference, which takes any f32. Reported here as a usage error, before any GPU work.
+    const std::pair<const char*, float> rate_args[] = {{"--b0 <RATE>", o.b0}, {"--b1 <RATE>", o.b1}, {"--d0 <RATE>", o.d0},
+                                                       {"--d1 <RATE>", o.d1}};
+    for (const auto& ra : rate_args)
+        if (!(ra.second == 0.f || (ra.second >= 0x1p-60f && ra.second <= 0x1p60f)))
+            usage_error("invalid value '" + std::to_string(ra.second) + "' for '" + ra.first +
+                        "': rates must be 0 or in [2^-60, 2^60] (8.67e-19 .. 1.15e18) for this engine");
     return o;
 }
 

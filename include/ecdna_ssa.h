@@ -43,7 +43,9 @@
 extern "C" {
 #endif
 
-#define ECDNA_SSA_ABI_VERSION 8
+/* ABI v9: draw mapping v7 (the channel from all 32 bits of the event's word over f64 cumulative propensities,
+ * DESIGN.md §3): same layout and entry points as v8, results differ from v8 seed for seed. */
+#define ECDNA_SSA_ABI_VERSION 9
 
 /* Process type — ProcessType (src/clap_app.rs:311-315); chosen as BirthDeath
  * when d0 > 0 or d1 > 0 (src/clap_app.rs:163-174, 194-200). */
@@ -128,8 +130,8 @@ typedef enum {
 
 /* Rates of one parameter set: ReactionRates([b0, b1, d0, d1]) (src/main.rs:67, 139). f32 as in Cli
  * (src/clap_app.rs:41-55). Each must be 0 or in [2^-60, 2^60] (else ECDNA_E_INVALID; the reference does not
- * check them; ABI v8): the f32 propensities of draw mapping v6 (rate x population, u32 populations) then stay
- * normal and finite, which the stepper's time-step division relies on. */
+ * check them; since ABI v8): the f32 propensities (rate x population, u32 populations) and the f32 total a0 of
+ * the time step then stay normal and finite, which the stepper's time-step division relies on. */
 typedef struct {
     float b0, b1, d0, d1;
 } ecdna_rates_t;
@@ -315,7 +317,7 @@ typedef struct {
     uint32_t bin_kmax;         /* bin store: binned copy numbers (0 for the other kernels) */
     uint32_t bin_c32;          /* bin store: 1 = u32 counters, 0 = u16 */
     uint32_t block_lanes;      /* workgroup size */
-    uint32_t blocks_per_cu;    /* resident workgroups per CU of the persistent grid */
+    uint32_t blocks_per_cu;    /* workgroups per CU of the launched grid (rounded up; largest chunk) */
     uint32_t cus;              /* compute units of the device */
     uint32_t n_chunks;         /* launches per run (HBM-bounded chunks) */
     uint32_t vgprs;            /* per lane, as compiled (hipFuncGetAttributes numRegs) */
@@ -323,7 +325,7 @@ typedef struct {
     uint32_t scratch_bytes;    /* private segment per lane */
     uint32_t window;           /* row store: 1 = LDS tail window variant */
     uint64_t chunk_replicates; /* replicates per chunk */
-    uint64_t grid_lanes;       /* lanes of the persistent grid */
+    uint64_t grid_lanes;       /* lanes of the launched grid (largest chunk; <= the occupancy cap) */
 } ecdna_ssa_instance_t;
 int ecdna_ssa_ctx_instance(const ecdna_ssa_ctx* c, ecdna_ssa_instance_t* out);
 int ecdna_ssa_ctx_destroy(ecdna_ssa_ctx* c);

@@ -47,6 +47,10 @@ def lib():
     L.oracle_philox4x32_10.restype = None
     L.oracle_softlog_neg.argtypes = [C.c_uint32]
     L.oracle_softlog_neg.restype = C.c_float
+    L.oracle_channel.argtypes = [P(C.c_float), C.c_uint64, C.c_uint64, C.c_int, C.c_uint32]
+    L.oracle_channel.restype = C.c_int
+    L.oracle_softlog_many.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p]
+    L.oracle_softlog_many.restype = None
     for fn in (L.oracle_run_philox, L.oracle_run_compat):
         fn.argtypes = [P(abi.Params), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int]
         fn.restype = C.c_int
@@ -103,6 +107,21 @@ def philox(ctr, key):
     o = (C.c_uint32 * 4)()
     lib().oracle_philox4x32_10(c, k, o)
     return list(o)
+
+
+def channel(rates, nminus: int, nplus: int, birth_death: bool, w1: int) -> int:
+    """The channel the engine's direct method draws with word w1 from (n-, n+) (draw mapping v7): 0 ProliferateNMinus,
+    1 ProliferateNPlus, 2 DeathNMinus, 3 DeathNPlus, -1 absorbing."""
+    r = (C.c_float * 4)(*[float(x) for x in rates])
+    return lib().oracle_channel(r, nminus, nplus, 1 if birth_death else 0, w1)
+
+
+def softlog_many(words) -> np.ndarray:
+    """oracle_softlog_neg over an array of u32 words (f32 results)."""
+    w = np.ascontiguousarray(words, dtype=np.uint32)
+    out = np.empty(len(w), dtype=np.float32)
+    lib().oracle_softlog_many(w.ctypes.data, len(w), out.ctypes.data)
+    return out
 
 
 def softlog_neg(w: int) -> float:

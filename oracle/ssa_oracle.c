@@ -25,9 +25,10 @@
  *
  * Floating point: compile with -ffp-contract=off. Every f32 / f64 operation
  * below is a correctly rounded IEEE add/sub/mul/div/fma in a fixed order (the
- * propensities, channel and time step in f32, draw mapping v6; the clock in
- * f64), so the HIP kernel (which spells the same operations with contraction
- * disabled) reproduces the times and channel picks bit for bit.
+ * propensities and time step in f32, the channel's cumulative sums and target
+ * in f64, draw mapping v7; the clock in f64), so the HIP kernel (which spells
+ * the same operations with contraction disabled) reproduces the times and
+ * channel picks bit for bit.
  */
 #include "ssa_oracle.h"
 #include "ssa_logtab.h"
@@ -75,7 +76,7 @@ void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t
 
 /* -------------------------------------------------------------- soft log */
 
-/* -ln(u), u = ((w >> 9) + 0.5) * 2^-23: the engine's draw mapping v6, in f32. d = (w >> 8) | 1
+/* -ln(u), u = ((w >> 9) + 0.5) * 2^-23: the engine's draw mapping (v6 and v7), in f32. d = (w >> 8) | 1
  * (odd, < 2^24: (float)d is exact) = m 2^ex with m in [0.5, 1) and u = d 2^-24; the top 7 fraction bits j of m
  * select {C, LN} = {RN32(1/mid_j), RN32(ln mid_j)} (ssa_logtab.h, tools/gen_logtab.py); r = fma(m, C, -1)
  * (|r| <= 2^-8); ln(1 + r) by a degree-4 series in explicit fmaf (C99 fmaf is the correctly rounded fused
@@ -101,9 +102,43 @@ float oracle_softlog_neg(uint32_t w) {
     return -fmaf(kf, ECDNA_LN2_HI, fmaf(kf, ECDNA_LN2_LO, ln + l));
 }
 
-/* The channel's uniform ((w >> 9) + 0.5) 2^-23 (exact; below 1 - 2^-24, so u a0 < a0 and a zero-propensity last
- * channel is never drawn). */
-static float chan_u(uint32_t w) { return fmaf((float)(w >> 9), 0x1p-23f, 0x1p-24f); }
+void oracle_softlog_many(const uint32_t* w, uint64_t n, float* out) {
+    for (uint64_t i = 0; i < n; ++i) out[i] = oracle_softlog_neg(w[i]);
+}
+
+/* The channel's target, draw mapping v7: u = (w + 0.5) 2^-32 from all 32 bits of w1 (exact in f64: one fma) times
+ * the f64 total propensity A, RN64. u <= 1 - 2^-33 keeps the target below A (a zero-propensity last channel is never
+ * drawn) and u >= 2^-33 keeps it above 0 (nor a zero-propensity first channel). */
+static double chan_target(uint32_t w, double A) { return fma((double)w, 0x1p-32, 0x1p-33) * A; }
+
+/* Propensities of update_state's population vector [n-, n+(, n-, n+)] (src/process.rs:187-196, 339-344) in f32, the
+ * reference's own (src/main.rs:67, 139); cumulative sums c[0..2] and the total *A in f64; returns a0 = RN32(A), the
+ * time step's divisor (draw mapping v7). */
+static float propensities(const float rates[4], uint64_t nminus, uint64_t nplus, int bd, double c[3], double* A) {
+    const float fnm = (float)nminus, fnp = (float)nplus;
+    float a[4];
+    a[0] = rates[0] * fnm;
+    a[1] = rates[1] * fnp;
+    a[2] = bd ? rates[2] * fnm : 0.0f;
+    a[3] = bd ? rates[3] * fnp : 0.0f;
+    c[0] = (double)a[0];
+    c[1] = c[0] + (double)a[1];
+    c[2] = c[1] + (double)a[2];
+    *A = c[2] + (double)a[3];
+    return (float)*A;
+}
+
+/* direct method: the channel is the number of cumulative propensities <= target */
+static int channel_of(const double c[3], double target) {
+    return target < c[0] ? 0 : (target < c[1] ? 1 : (target < c[2] ? 2 : 3));
+}
+
+int oracle_channel(const float rates[4], uint64_t nminus, uint64_t nplus, int birth_death, uint32_t w1) {
+    double c[3], A;
+    const float a0 = propensities(rates, nminus, nplus, birth_death, c, &A);
+    if (!(a0 > 0.0f)) return -1;
+    return channel_of(c, chan_target(w1, A));
+}
 
 /* ------------------------------------------------------------ word stream */
 
@@ -533,17 +568,11 @@ static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16
             stop = ECDNA_STOP_MAX_TIME;
             break;
         }
-        /* propensities rate_i * population_i, population = update_state's vector; f32 (draw mapping v6) */
-        const float fnm = (float)nminus, fnp = (float)nplus;
-        float a[4];
-        a[0] = rt.b0 * fnm;
-        a[1] = rt.b1 * fnp;
-        a[2] = bd ? rt.d0 * fnm : 0.0f;
-        a[3] = bd ? rt.d1 * fnp : 0.0f;
-        float c0 = a[0];
-        float c1 = c0 + a[1];
-        float c2 = c1 + a[2];
-        float a0 = c2 + a[3];
+        /* propensities rate_i * population_i, population = update_state's vector, in f32 (the reference's own,
+         * src/main.rs:67, 139); their cumulative sums in f64 and the time step's total a0 = RN32(A) (draw mapping v7) */
+        const float rates4[4] = {rt.b0, rt.b1, rt.d0, rt.d1};
+        double c[3], A;
+        const float a0 = propensities(rates4, nminus, nplus, bd, c, &A);
         if (!(a0 > 0.0f)) {
             stop = ECDNA_STOP_ABSORBING;
             break;
@@ -560,8 +589,7 @@ static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16
         uint32_t w[4];
         event_block(p->seed, rid, e, w);
         /* direct method: channel by w1 against the cumulative propensities */
-        float target = chan_u(w[1]) * a0;
-        int ch = target < c0 ? 0 : (target < c1 ? 1 : (target < c2 ? 2 : 3));
+        const int ch = channel_of(c, chan_target(w[1], A));
         float tau = oracle_softlog_neg(w[0]) / a0; /* the correctly rounded f32 quotient */
         wstream ws;
         ws_init(&ws, p->seed, rid, e, w[2], w[3]);

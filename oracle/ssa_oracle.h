@@ -34,6 +34,12 @@ extern "C" {
 void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 /* -ln(((w >> 9) + 0.5) * 2^-23) by the engine's fixed-operation-order f32 software log (draw mapping v6). */
 float oracle_softlog_neg(uint32_t w);
+/* out[i] = oracle_softlog_neg(w[i]) for i < n (the time draw's whole law in one call: tests/test_mapping_v7.py). */
+void oracle_softlog_many(const uint32_t* w, uint64_t n, float* out);
+/* The channel the direct method draws with word w1 from the state (n-, n+) under rates {b0, b1, d0, d1} (draw mapping
+ * v7: f32 propensities, f64 cumulative sums, target (w1 + 0.5) 2^-32 A): 0 ProliferateNMinus, 1 ProliferateNPlus,
+ * 2 DeathNMinus, 3 DeathNPlus; -1 when every propensity is 0. Pure birth: birth_death = 0 (d0, d1 ignored). */
+int oracle_channel(const float rates[4], uint64_t nminus, uint64_t nplus, int birth_death, uint32_t w1);
 
 /* ---- whole runs ---- */
 /* Same contract as ecdna_ssa_run (include/ecdna_ssa.h) with host buffers; out_rows, if given,

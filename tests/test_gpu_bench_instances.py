@@ -129,3 +129,47 @@ def test_c3_bench_instance_bit_exact(engine_mod, oracle_mod):
     assert ins["rotation"] == 1 and ins["runtime_flags"] == 0 and ins["blocks_per_cu"] == 4, ins
     for local in (0, 333_333, (1 << 20) - 256):
         _compare_sample(res, spec, oracle_mod, local, 256)
+
+
+@pytest.mark.gpu
+def test_c3_strong_8gpu_shard_instance_bit_exact(engine_mod, oracle_mod):
+    """The metric's fixed-total reading at 8 GPUs (bench.py --scaling strong --gpus 8): rank 7's contiguous 1/8 of 2^20
+    replicates (131,072, ids 917,504 .. 2^20 - 1; K = 32 / u32): half a replicate per lane of the four-workgroup grid, so
+    the launch is 512 workgroups (two per CU, grid_lanes = the replicates) under the max-ILP schedule (at most one wave
+    of replicates per SIMD... two here: 256 replicates per CU), unpaired (birth-death with more than half a wave per
+    SIMD), no rotation; samples equal the oracle."""
+    bench = _bench()
+    first, n = shard.shard_range(7, 8, 1 << 20)
+    assert (first, n) == (917_504, 131_072)
+    spec = bench.workload_spec(first, n, 1 << 20, workload="c3")
+    assert spec.bin_kmax == 32 and spec.flags == abi.FLAG_BIN_STORE
+    ins, res = _run_with_instance(engine_mod, spec)
+    assert (ins["kernel"], ins["schedule"], ins["paired"], ins["bin_kmax"], ins["bin_c32"]) == (1, 1, 0, 32, 1), ins
+    assert ins["rotation"] == 0 and ins["runtime_flags"] == 0 and ins["n_chunks"] == 1, ins
+    assert ins["grid_lanes"] == 131_072 and ins["blocks_per_cu"] == 2, ins  # the launched grid (ADVICE r04)
+    assert np.all(res.summaries["error"] == 0) and int(res.totals["replicates"][0]) == n
+    for local in (0, 65_536, n - 256):
+        _compare_sample(res, spec, oracle_mod, local, 256)
+
+
+@pytest.mark.gpu
+def test_instance_reports_the_launched_grid_of_an_underfilled_paired_run(engine_mod):
+    """the instance names the grid actually launched, not the occupancy cap. A C5-shaped paired run of 8,192
+    replicates launches ceil(8192 / 128 owners) = 64 workgroups of 256 lanes; a 1,000-replicate unpaired pure-birth run
+    4 workgroups; ECDNA_SSA_MAX_BLOCKS caps both."""
+    spec = abi.RunSpec(seed=1, process=abi.BIRTH_DEATH, rates=((1.0, 1.0, 0.9, 0.9),), n_replicates=8192, max_cells=2000,
+                       max_time=5.0, init={1: 1000}, flags=abi.FLAG_BIN_STORE, bin_kmax=64)
+    with engine_mod.Context(spec) as ctx:
+        ins = ctx.instance()
+    assert ins["paired"] == 1 and ins["grid_lanes"] == 64 * 256 and ins["blocks_per_cu"] == 1, ins
+    spec2 = abi.RunSpec(seed=1, n_replicates=1000, max_cells=100, flags=abi.FLAG_BIN_STORE, bin_kmax=32)
+    with engine_mod.Context(spec2) as ctx:
+        ins2 = ctx.instance()
+    assert ins2["paired"] == 0 and ins2["grid_lanes"] == 4 * 256, ins2
+    os.environ["ECDNA_SSA_MAX_BLOCKS"] = "16"
+    try:
+        with engine_mod.Context(spec) as ctx:
+            ins3 = ctx.instance()
+    finally:
+        del os.environ["ECDNA_SSA_MAX_BLOCKS"]
+    assert ins3["grid_lanes"] == 16 * 256, ins3

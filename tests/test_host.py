@@ -74,6 +74,16 @@ def test_cli_years_from_cells(host, cells, years):
     assert dry("--cells", str(cells))["years"] == years
 
 
+@pytest.mark.parametrize("flag,value", [("--b0", "1e-20"), ("--b1", "1e30"), ("--d0", "-1"), ("--d1", "inf")])
+def test_cli_rate_outside_the_engine_range_is_a_usage_error(host, flag, value):
+    """The engine takes rates 0 or in [2^-60, 2^60] (include/ecdna_ssa.h, since ABI v8), a divergence from the
+    reference's any-f32 clap values: reported before any GPU work, exit code 2."""
+    out = subprocess.run([CLI, "--dry-run", flag, value, "/tmp/ecdna_out"], capture_output=True, text=True)
+    assert out.returncode == 2 and "2^-60, 2^60" in out.stderr, out.stderr
+    for ok in ("0", "1e-18", "1e18"):
+        assert subprocess.run([CLI, "--dry-run", flag, ok, "/tmp/ecdna_out"], capture_output=True).returncode == 0
+
+
 def test_cli_process_type_from_death_rates(host):
     # is_birth_death = d0 > 0 | d1 > 0 (src/clap_app.rs:163-174)
     assert dry("--d0", "0", "--d1", "0")["process"] == "PureBirth"

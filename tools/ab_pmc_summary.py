@@ -1,5 +1,5 @@
 """SQ instruction counts per wave-event of the bin stepper from one rocprofv3 --pmc pass over a 1-step bench
-(tools/r04_ab.sh). Development tool. Usage: python tools/ab_pmc_summary.py <pmc dir> <bench stdout> <name>"""
+(tools/gpu_session.sh, step pmc). Development tool. Usage: python tools/ab_pmc_summary.py <pmc dir> <bench stdout> <name>"""
 import csv
 import glob
 import json

@@ -1,0 +1,71 @@
+#!/bin/bash
+# One GPU session, assembled from steps (the reusable A/B driver; replaces round 4's one-off tools/r04_*.sh).
+#   STEPS   comma list, run in order (default: suite,ab_c3,latency):
+#     suite      the full -m gpu suite on the working tree's library
+#     parity     the parity subset only (parity, random parity, rotation, drain, rare channels)
+#     ab_c3      C3 (K = 32) with each prebuilt library of LIBS, interleaved twice (tools/ab_libs.sh)
+#     latency    C2, C4 rank-0 shard, C5 rank-0 shard with each library (tools/ab_latency.sh)
+#     pmc        one SQ-counter pass (VALU / SALU / LDS per wave-event of one C3 step) per library
+#     c3s        the C3 fixed-total shards (G = 1, 2, 4, 8; all ranks) with the working tree (tools/c3_strong.py)
+#     c3s_knobs  launch knobs on the C3 fixed-total rank-0 shards (G = 2, 4, 8)
+#     c4s        the eight C4 8-GPU shards one after another (tools/c4_shards.sh)
+#   LIBS    prebuilt libraries ecdna-evo_amd/lib_ab/<name>/ (tools/ab_build.sh <ref|WORKTREE> <name>)
+#   TAG     prefix of the outputs under gpurun_out/
+# Usage: STEPS=parity,ab_c3 LIBS="base new" TAG=r05x bash tools/gpu_session.sh
+set -euo pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+STEPS=${STEPS:-suite,ab_c3,latency}
+LIBS=${LIBS:-}
+TAG=${TAG:-sess}
+export ECDNA_SSA_ABI_ANY=1  # (A/B libraries of an earlier ABI with the same layout)
+L=$PWD/ecdna-evo_amd/lib_ab
+for step in ${STEPS//,/ }; do
+  echo "== $step"
+  case $step in
+    suite)
+      timeout -k 10 700 python3 -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread \
+        > gpurun_out/${TAG}_gpu_suite.txt 2>&1 || { echo SUITE FAILED; tail -40 gpurun_out/${TAG}_gpu_suite.txt; exit 1; }
+      tail -1 gpurun_out/${TAG}_gpu_suite.txt ;;
+    parity)
+      timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_random_parity.py \
+        tests/test_gpu_rotation.py tests/test_gpu_drain.py tests/test_gpu_rare_channels.py -q -x --timeout 300 \
+        --timeout-method thread > gpurun_out/${TAG}_parity.txt 2>&1 || { echo PARITY FAILED; tail -30 gpurun_out/${TAG}_parity.txt; exit 1; }
+      tail -1 gpurun_out/${TAG}_parity.txt ;;
+    ab_c3)
+      bash tools/ab_libs.sh $LIBS 2>&1 | grep "^{" | tee gpurun_out/${TAG}_ab_c3.txt ;;
+    latency)
+      bash tools/ab_latency.sh $LIBS 2>&1 | tail -$((6 * $(echo $LIBS | wc -w))) | tee gpurun_out/${TAG}_ab_latency.txt ;;
+    pmc)
+      for n in $LIBS; do
+        ECDNA_SSA_LIB=$L/$n/libecdna_ssa.so timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS \
+          SQ_WAVES SQ_BUSY_CYCLES -T --output-format csv -d gpurun_out/${TAG}_pmc_$n -o pmc -- python3 bench.py --steps 1 \
+          --warmup 0 --no-cpu-baseline > gpurun_out/${TAG}_pmc_$n.log 2>&1
+        python3 tools/ab_pmc_summary.py gpurun_out/${TAG}_pmc_$n gpurun_out/${TAG}_pmc_$n.log "$n" | tee -a gpurun_out/${TAG}_pmc.txt
+      done ;;
+    c3s)
+      timeout -k 10 300 python3 -u tools/c3_strong.py > gpurun_out/${TAG}_c3_strong.jsonl 2> gpurun_out/${TAG}_c3_strong.err
+      grep makespan gpurun_out/${TAG}_c3_strong.jsonl ;;
+    c3s_knobs)
+      O=gpurun_out/${TAG}_c3_strong_knobs.txt; : > $O
+      knob() {  # label, env...
+        local label=$1; shift
+        env "$@" C3S_RANKS=0 C3S_REPS=3 timeout -k 10 200 python3 tools/c3_strong.py 2>/dev/null | python3 -c "
+import json,sys
+for l in sys.stdin:
+    d=json.loads(l)
+    if 'best_ms' in d: i=d['instance']; print('$label', 'G=%d' % d['gpus'], d['best_ms'], d['stepper_ms'], 'sched', i['schedule'], 'rot', i['rotation'], 'drain', i['drain_control'], 'bpc', i['blocks_per_cu'], 'K', i['bin_kmax'])
+" >> $O
+      }
+      knob auto C3S_GPUS=2,4,8
+      knob rot1 C3S_GPUS=2,4 ECDNA_SSA_ROTATE=1
+      knob rot1min1 C3S_GPUS=2,4 ECDNA_SSA_ROTATE=1 ECDNA_SSA_ROT_PARK_MIN=1
+      knob sched0 C3S_GPUS=2,4,8 ECDNA_SSA_SCHED=0
+      knob k64 C3S_GPUS=2,4,8 PROBE_KMAX=64
+      knob admit8 C3S_GPUS=2 ECDNA_SSA_ADMIT_X8=8
+      cat $O ;;
+    c4s)
+      bash tools/c4_shards.sh | tee gpurun_out/${TAG}_c4_shards.txt ;;
+    *) echo "unknown step $step"; exit 1 ;;
+  esac
+done

@@ -1,6 +1,7 @@
 """Throughput of the engine on every BASELINE.json config shape that runs on one GPU
 (configs[1..4]; C4 and C5 as the per-GPU shard of their 8-GPU runs). Development/measurement tool.
-Usage: [PROBE_FLAGS=0x20] [PROBE_KMAX=256] [PROBE_SEG=s] [PROBE_RANK=r] [PROBE_GPUS=8] python tools/probe_configs.py [c2 c3 c4 c5]"""
+c3s = the metric's fixed-total C3 reading (2^20 replicates over PROBE_GPUS GPUs), shard PROBE_RANK.
+Usage: [PROBE_FLAGS=0x20] [PROBE_KMAX=256] [PROBE_SEG=s] [PROBE_RANK=r] [PROBE_GPUS=8] python tools/probe_configs.py [c2 c3 c4 c5 c3s]"""
 import dataclasses
 import json
 import os
@@ -55,19 +56,29 @@ def c5_shard(rank=0, gpus=8):
                        init={1: 1000}, hist_bins=1025, flags=0, big_cap=int(os.environ.get("PROBE_BIG_CAP", 1 << 16)))
 
 
+def c3_strong_shard(rank=0, gpus=8):
+    """The metric's fixed-total reading of C3: 2^20 replicates in total, rank `rank` of `gpus` runs the contiguous
+    ids [rank 2^20 / gpus, (rank + 1) 2^20 / gpus) (bench.py --scaling strong)."""
+    total = 1 << 20
+    first, last = rank * total // gpus, (rank + 1) * total // gpus
+    return abi.RunSpec(seed=42, process=abi.BIRTH_DEATH, rates=((1.0, 1.5, 0.3, 0.3),), reps_per_set=total,
+                       first_replicate=first, n_replicates=last - first, max_cells=10_000, hist_bins=1025, flags=0)
+
+
 CONFIGS = {
     "c2": lambda: abi.RunSpec(seed=42, n_replicates=65536, max_cells=10_000, flags=0),
     "c3": lambda: abi.RunSpec(seed=42, process=abi.BIRTH_DEATH, rates=((1.0, 1.5, 0.3, 0.3),),
                               n_replicates=1 << 20, max_cells=10_000, flags=0),
     "c4": c4_shard,
     "c5": c5_shard,
+    "c3s": c3_strong_shard,
 }
 
 
 def main():
     for name in sys.argv[1:] or list(CONFIGS):
         gpus = int(os.environ.get("PROBE_GPUS", "8"))  # the layout the shard belongs to (1: the whole config)
-        spec = CONFIGS[name](int(os.environ.get("PROBE_RANK", "0")), gpus) if name in ("c4", "c5") else CONFIGS[name]()
+        spec = CONFIGS[name](int(os.environ.get("PROBE_RANK", "0")), gpus) if name in ("c4", "c5", "c3s") else CONFIGS[name]()
         spec = dataclasses.replace(spec, flags=spec.flags | int(os.environ.get("PROBE_FLAGS", "0"), 0),
                                    bin_kmax=int(os.environ.get("PROBE_KMAX", "0")), _keep=[])
         if "PROBE_SEG" in os.environ:  # another segregation rule (abi.SEG_*) on the same shape
@@ -85,7 +96,7 @@ def main():
         ev = int(t["events"].sum())
         print(json.dumps({"config": name, "flags": spec.flags, "bin_kmax": spec.bin_kmax, "replicates": spec.n_replicates, "events": ev, "stepper_ms": s_ms,
                           "hist_ms": h_ms, "wall_ms": wall * 1e3, "events_per_s_kernel": ev / (s_ms * 1e-3),
-                          "events_per_s_wall": ev / wall, "geometry": ctx.geometry(),
+                          "events_per_s_wall": ev / wall, "geometry": ctx.geometry(), "instance": ctx.instance(),
                           "stops": t["stop_reasons"].sum(axis=0).tolist(), "errors": int(t["errors"].sum()),
                           "setup_s": t1 - t0}), flush=True)
         ctx.close()
