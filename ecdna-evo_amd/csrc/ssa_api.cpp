@@ -229,6 +229,9 @@ struct ecdna_ssa_ctx {
 
 namespace {
 
+// the flags the kernels see: the caller's, plus the internal snapshot bit that selects the runtime-flags instances
+uint32_t kernel_flags(const ecdna_ssa_params_t& p) { return p.flags | (p.n_snapshots ? ecdna::kFlagSnapshotsRt : 0u); }
+
 int pick_device(int dev) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(ECDNA_E_NODEVICE, "no HIP device");
@@ -528,10 +531,11 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
         // ECDNA_SSA_SCHED = 0 default, 1 max-ILP, 2 auto, 3 the 128-VGPR build (K = 64 / u16; else 0).
         uint64_t max_chunk = 0;
         for (const auto& ch : c->chunks) max_chunk = std::max<uint64_t>(max_chunk, ch.n);
+        const uint32_t kflags = kernel_flags(*p);
         const uint64_t sched = env_u64("ECDNA_SSA_SCHED", 2);
         // (auto only without f32 time and the event hash: that variant spills 12 B at 128 VGPRs)
         const bool k64u16 = c->bin_k == 64 && !c->bin_c32;
-        const bool tf0 = (p->flags & (ECDNA_FLAG_TIME_F32 | ECDNA_FLAG_EVENT_HASH)) == 0;
+        const bool tf0 = (kflags & ecdna::kRuntimeFlagMask) == 0;
         // Where the max-ILP build keeps the default's occupancy (LDS bounds both: K = 32 / u32 and K = 64 / u32
         // since the f32 draw mapping v6, K = 256) it is taken too: its schedule then costs no lanes (C3 78.3 ->
         // 77.3 ms, C5 whole 31.9 -> 30.4 s, same box). With fewer than four replicates per lane of the default
@@ -540,20 +544,23 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
         // latency-bound (profiles/r04d_v6_suite_and_sched_sweep.txt).
         int occ_def = 0, occ_ilp = 0;
         CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ_def, ecdna::bin_stepper_kernel(p->process, p->segregation, c->bin_k, c->bin_c32, p->flags, 0),
+            &occ_def, ecdna::bin_stepper_kernel(p->process, p->segregation, c->bin_k, c->bin_c32, kflags, 0),
             (int)c->stepper_block, 0));
         CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ_ilp, ecdna::bin_stepper_kernel(p->process, p->segregation, c->bin_k, c->bin_c32, p->flags, 1),
+            &occ_ilp, ecdna::bin_stepper_kernel(p->process, p->segregation, c->bin_k, c->bin_c32, kflags, 1),
             (int)c->stepper_block, 0));
         // Paired lanes: with at most half a wave of replicates per SIMD (the C5 8-GPU shard) the
         // idle half of each wave computes the next event's Philox block and soft log in the N- fast-forward.
         // Birth-death without snapshots (the fast-forward's domain). ECDNA_SSA_PAIR = 0 off, 1 whenever
         // possible, 2 auto.
+        // Quads (ECDNA_SSA_PAIR = 3 whenever possible): four lanes per replicate, four events per fast-forward step.
         const uint64_t pair_mode = env_u64("ECDNA_SSA_PAIR", 2);
         const bool pair_ok = p->process == ECDNA_BIRTH_DEATH && p->n_snapshots == 0 &&
-                             ecdna::bin_stepper_kernel_pair(p->segregation, c->bin_k, c->bin_c32, p->flags) != nullptr;
-        if (pair_ok && (pair_mode == 1 ||
-                        (pair_mode == 2 && sched == 2 && max_chunk <= (uint64_t)c->cus * (ecdna::kStepperBlock / 2))))
+                             ecdna::bin_stepper_kernel_pair(p->segregation, c->bin_k, c->bin_c32, kflags, 2) != nullptr;
+        if (pair_ok && pair_mode == 3)
+            c->bin_ilp = 4;
+        else if (pair_ok && (pair_mode == 1 ||
+                             (pair_mode == 2 && sched == 2 && max_chunk <= (uint64_t)c->cus * (ecdna::kStepperBlock / 2))))
             c->bin_ilp = 3;
         else if (sched == 1 || (sched == 2 && max_chunk <= (uint64_t)c->cus * 256u))
             c->bin_ilp = 1;
@@ -566,7 +573,7 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
         // bin store: LDS-resident events, bounded by issue and LDS latency: every resident block helps
         CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &per_cu,
-            ecdna::bin_stepper_kernel(p->process, p->segregation, c->bin_k, c->bin_c32, p->flags, c->bin_ilp),
+            ecdna::bin_stepper_kernel(p->process, p->segregation, c->bin_k, c->bin_c32, kflags, c->bin_ilp),
             (int)c->stepper_block, 0));
     } else {
         CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -636,7 +643,9 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
     // replicates once fewer than 1.5 grids' worth are left (C3: 105 -> 101 ms). ECDNA_SSA_ADMIT=0:
     // off. Rotation replaces it.
     for (auto& ch : c->chunks) {
-        const uint32_t per_block = c->bin_ilp == 3 ? c->stepper_block / 2 : c->stepper_block;  // (paired: owners)
+        // (paired lanes: owners only)
+        const uint32_t per_block =
+            c->bin_ilp == 3 ? c->stepper_block / 2 : (c->bin_ilp == 4 ? c->stepper_block / 4 : c->stepper_block);
         const uint32_t need = (ch.n + per_block - 1) / per_block;
         ch.blocks = std::max<uint32_t>(1, std::min<uint32_t>(need, c->stepper_blocks_cap));
         const uint64_t lanes = (uint64_t)ch.blocks * c->stepper_block;
@@ -699,7 +708,7 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
         a.init_nplus = p.init_nplus;
         a.max_iter = (uint32_t)p.max_iter;
         a.cell_cap = p.cell_cap;
-        a.flags = p.flags;
+        a.flags = kernel_flags(p);  // (with the internal snapshot bit: it selects the kernel instance)
         // (n- + n+) * 2 >= max_cells  <=>  n- + n+ >= ceil(max_cells / 2)
         a.stop_cells = (p.process == ECDNA_BIRTH_DEATH && (p.flags & ECDNA_FLAG_BD_CAP_COMPAT))
                            ? p.max_cells / 2 + (p.max_cells & 1)
@@ -823,11 +832,11 @@ int ecdna_ssa_ctx_instance(const ecdna_ssa_ctx* c, ecdna_ssa_instance_t* out) {
     } else if (c->bin_k) {
         r.kernel = ECDNA_KERNEL_BINS;
         r.schedule = c->bin_ilp;
-        r.paired = c->bin_ilp == 3 ? 1 : 0;
+        r.paired = c->bin_ilp == 3 ? 1 : (c->bin_ilp == 4 ? 2 : 0);
         r.bin_kmax = c->bin_k;
         r.bin_c32 = (uint32_t)c->bin_c32;
-        r.runtime_flags = (p.flags & (ECDNA_FLAG_TIME_F32 | ECDNA_FLAG_EVENT_HASH)) ? 1 : 0;
-        fn = ecdna::bin_stepper_kernel(p.process, p.segregation, c->bin_k, c->bin_c32, p.flags, c->bin_ilp);
+        r.runtime_flags = (kernel_flags(p) & ecdna::kRuntimeFlagMask) ? 1 : 0;
+        fn = ecdna::bin_stepper_kernel(p.process, p.segregation, c->bin_k, c->bin_c32, kernel_flags(p), c->bin_ilp);
     } else {
         r.kernel = ECDNA_KERNEL_ROWS;
         r.schedule = -1;

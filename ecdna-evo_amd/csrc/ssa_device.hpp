@@ -147,7 +147,12 @@ __device__ __forceinline__ float softlog_neg(uint32_t w, const float2* tab) { re
 // below A and a last channel of zero propensity is never drawn; u >= 2^-33 and A >= 2^-60 keep it above 0, so a first
 // channel of zero propensity is never drawn either. (v6 took 23 bits of w1 and f32 cumulative sums: a channel below
 // ~2^-24 of the total could not fire)
-__device__ __forceinline__ double chan_target(uint32_t w, double a) { return fma((double)w, 0x1p-32, 0x1p-33) * a; }
+//
+// Formed as ((w + 0.5) A) 2^-32: one conversion, one add of the inline constant 0.5 and two multiplies (the second by
+// a power of two, exact: the product stays far above the f64 underflow), no f64 constant to materialise in registers;
+// RN((w + 0.5) A) 2^-32 = RN((w + 0.5) 2^-32 A), the oracle's u A, bit for bit. (Host-callable: the CPU tests check it
+// against the oracle's channel function, tests/native/device_math_check.cpp.)
+__host__ __device__ __forceinline__ double chan_target(uint32_t w, double a) { return ((double)w + 0.5) * a * 0x1p-32; }
 
 // n / d, the correctly rounded IEEE f32 quotient (the oracle's C division), for operands in the stepper's range.
 // LLVM lowers an f32 divide to v_div_scale x2, v_rcp_f32, the Newton step, the quotient and two residual

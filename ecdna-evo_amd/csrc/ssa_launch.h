@@ -108,6 +108,11 @@ constexpr int kBinWideBlock = 64;  // bin store with 256 bins
 constexpr int kHistBlock = 256;
 constexpr uint32_t kMaxHistBins = 4096;  // LDS: 8 B per bin per workgroup (<= 64 KiB)
 constexpr uint32_t kMaxSnapshots = 64;
+// Internal flag bit (never a user flag): the run takes snapshots. With f32 time and the event hash it selects the bin
+// stepper's runtime-flags instances (TF = 1); the TF = 0 instances (the bench's) compile snapshots, f32 time and the
+// hash out, which frees the scalar registers the snapshot test held across the event loop.
+constexpr uint32_t kFlagSnapshotsRt = 0x80000000u;
+constexpr uint32_t kRuntimeFlagMask = ECDNA_FLAG_TIME_F32 | ECDNA_FLAG_EVENT_HASH | kFlagSnapshotsRt;
 
 // Kernel handle for occupancy queries and the launch itself.
 // window: 1 = LDS tail window variant (default), 0 = rows straight in HBM (A/B reference)
@@ -126,8 +131,9 @@ const void* bin_stepper_kernel(int birth_death, int segregation, uint32_t bin_k,
 const void* bin_stepper_kernel_ilp(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags);
 // ilp = 3: the max-ILP schedule with paired lanes (lane l < 32 owns a replicate, lane l + 32 helps its N-
 // fast-forward; birth-death, K = 32 / u32 or K = 64): nullptr where no such instance exists. A paired
-// workgroup of kStepperBlock lanes runs kStepperBlock / 2 replicates at a time.
-const void* bin_stepper_kernel_pair(int segregation, uint32_t bin_k, int c32, uint32_t flags);
+// workgroup of kStepperBlock lanes runs kStepperBlock / 2 replicates at a time. ilp = 4: quads (lane 4j owns a
+// replicate, lanes 4j + 1 .. 4j + 3 help): kStepperBlock / 4 replicates per workgroup. group: 2 or 4.
+const void* bin_stepper_kernel_pair(int segregation, uint32_t bin_k, int c32, uint32_t flags, int group);
 int bin_stepper_block(uint32_t bin_k);
 hipError_t launch_bin_stepper(const StepperArgs& a, int birth_death, int segregation, uint32_t bin_k, int c32, int ilp,
                               uint32_t blocks, hipStream_t stream);

@@ -103,7 +103,8 @@ FLAG_REFERENCE_DRAWS = 0x40
 
 # ecdna_ssa_instance_t (ABI v7): the kernel instance a context launches (ecdna_ssa_ctx_instance)
 KERNEL_KINDS = {0: "ssa_stepper (rows)", 1: "ssa_stepper_bins (bins)", 2: "ssa_stepper_refdraws (reference draws)"}
-SCHEDULE_NAMES = {-1: "n/a", 0: "occupancy-first", 1: "max-ILP", 2: "occupancy-first, 128-VGPR cap", 3: "max-ILP, paired lanes"}
+SCHEDULE_NAMES = {-1: "n/a", 0: "occupancy-first", 1: "max-ILP", 2: "occupancy-first, 128-VGPR cap", 3: "max-ILP, paired lanes",
+                  4: "max-ILP, lane quads"}
 
 
 class Instance(C.Structure):

@@ -307,13 +307,16 @@ typedef enum {
 typedef struct {
     int32_t kernel;            /* ecdna_kernel_kind_t */
     int32_t schedule;          /* bin stepper: 0 occupancy-first, 1 max-ILP, 2 occupancy-first capped at 128
-                                  VGPRs (K = 64 / u16), 3 max-ILP with paired lanes; -1 for the other kernels */
-    int32_t paired;            /* 1: lane l < 32 owns a replicate, lane l + 32 helps its N- fast-forward */
+                                  VGPRs (K = 64 / u16), 3 max-ILP with paired lanes, 4 max-ILP with quads; -1 for
+                                  the other kernels */
+    int32_t paired;            /* 1: lane l < 32 owns a replicate, lane l + 32 helps its N- fast-forward (pairs);
+                                  2: lane 4j owns one, lanes 4j + 1 .. 4j + 3 help (quads) */
     int32_t rotation;          /* number of chunks whose replicates rotate through the lanes */
     int32_t rot_tick_log2;     /* rotation tick (loop iterations, log2) */
     int32_t drain_control;     /* number of chunks whose youngest wave slots stop admitting replicates early */
     int32_t cost_order;        /* 1: replicates start costliest set first (params.set_cost_hint) */
-    int32_t runtime_flags;     /* 1: the instance reads f32 time / event hash from the flags (TF = 1) */
+    int32_t runtime_flags;     /* 1: the instance reads f32 time, the event hash and snapshots from its arguments
+                                  (TF = 1); 0: compiled out */
     uint32_t bin_kmax;         /* bin store: binned copy numbers (0 for the other kernels) */
     uint32_t bin_c32;          /* bin store: 1 = u32 counters, 0 = u16 */
     uint32_t block_lanes;      /* workgroup size */

@@ -1,0 +1,100 @@
+// TEST INFRASTRUCTURE ONLY — host-side check of the stepper header's host-callable draw-mapping pieces
+// (ecdna-evo_amd/csrc/ssa_device.hpp) against the CPU oracle's channel function (oracle/ssa_oracle.c:136,
+// oracle_channel), built with hipcc and run on the CPU by tests/test_mapping_v7.py.
+//
+// The propensity / cumulative-sum sequence below is the one the steppers inline (ssa_kernels.hip, ssa_stepper
+// "propensities" block): f32 products rate * f32(pop), f64 cumulative sums, then chan_target(w1, A) against the
+// boundaries. chan_target itself is the header's function, so a change of its scale or rounding that the oracle
+// does not share shows here, without a GPU.
+// Prints "cases=<n> mismatches=<m>" and exits 1 on any mismatch.
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "ssa_device.hpp"
+
+extern "C" int oracle_channel(const float rates[4], uint64_t nminus, uint64_t nplus, int birth_death, uint32_t w1);
+
+namespace {
+
+uint64_t g_state = 0x9E3779B97F4A7C15ull;
+uint64_t next_u64() {  // splitmix64
+    uint64_t z = (g_state += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+float rand_rate() {  // 0 or log-uniform in [2^-60, 2^60], the range ecdna_ssa_ctx_create accepts
+    const uint64_t r = next_u64();
+    if ((r & 7u) == 0u) return 0.0f;
+    const double ex = -60.0 + 120.0 * (double)(r >> 11) * 0x1p-53;
+    return (float)exp2(ex);
+}
+
+uint32_t rand_pop() {
+    const uint64_t r = next_u64();
+    switch (r & 3u) {
+        case 0: return 0u;
+        case 1: return (uint32_t)((r >> 8) & 15u);
+        case 2: return (uint32_t)((r >> 8) & 0xFFFFu);
+        default: return (uint32_t)(r >> 32);
+    }
+}
+
+int kernel_channel(const float r[4], uint32_t nm, uint32_t np, bool bd, uint32_t w1) {
+    const float fnm = (float)nm, fnp = (float)np;
+    const double cA = (double)(r[0] * fnm);
+    const double cB = cA + (double)(r[1] * fnp);
+    double cC = cB, A = cB;
+    if (bd) {
+        cC = cB + (double)(r[2] * fnm);
+        A = cC + (double)(r[3] * fnp);
+    }
+    if (!((float)A > 0.0f)) return -1;
+    const double target = ecdna::chan_target(w1, A);
+    if (bd) return target < cA ? 0 : (target < cB ? 1 : (target < cC ? 2 : 3));
+    return target < cA ? 0 : 1;
+}
+
+}  // namespace
+
+int main() {
+    long cases = 0, bad = 0;
+    for (int i = 0; i < 200000; ++i) {
+        const float r[4] = {rand_rate(), rand_rate(), rand_rate(), rand_rate()};
+        const uint32_t nm = rand_pop(), np = rand_pop();
+        const bool bd = (i & 1) != 0;
+        // w1: random, the extremes, and the words either side of each boundary
+        uint32_t ws[12];
+        int nw = 0;
+        ws[nw++] = (uint32_t)next_u64();
+        ws[nw++] = 0u;
+        ws[nw++] = 0xFFFFFFFFu;
+        const float fnm = (float)nm, fnp = (float)np;
+        const double c0 = (double)(r[0] * fnm), c1 = c0 + (double)(r[1] * fnp);
+        const double c2 = c1 + (bd ? (double)(r[2] * fnm) : 0.0);
+        const double A = c2 + (bd ? (double)(r[3] * fnp) : 0.0);
+        if (A > 0.0) {
+            for (double c : {c0, c1, c2}) {
+                const double w = floor(c / A * 0x1p32 - 0.5);
+                for (int d = -1; d <= 1; ++d) {
+                    const double x = w + d;
+                    if (x >= 0.0 && x <= 4294967295.0 && nw < 12) ws[nw++] = (uint32_t)x;
+                }
+            }
+        }
+        for (int k = 0; k < nw; ++k) {
+            const int want = oracle_channel(r, nm, np, bd ? 1 : 0, ws[k]);
+            const int got = kernel_channel(r, nm, np, bd, ws[k]);
+            ++cases;
+            if (want != got) {
+                if (++bad <= 5)
+                    fprintf(stderr, "mismatch: rates %a %a %a %a nm %u np %u bd %d w1 %u: oracle %d header %d\n",
+                            r[0], r[1], r[2], r[3], nm, np, bd ? 1 : 0, ws[k], want, got);
+            }
+        }
+    }
+    printf("cases=%ld mismatches=%ld\n", cases, bad);
+    return bad ? 1 : 0;
+}

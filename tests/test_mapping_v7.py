@@ -16,6 +16,9 @@ second moment and the tail masses P(X > x). (The total variation distance betwee
 any discretization, so it does not measure the draw; the KS distance does.) The reference draws Exp1 by the
 ziggurat from 64-bit words and casts to f32 (rand_distr 0.4.3)."""
 import math
+import os
+import shutil
+import subprocess
 from fractions import Fraction
 
 import numpy as np
@@ -23,6 +26,7 @@ import pytest
 
 f32 = np.float32
 TWO32 = 1 << 32
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 # ------------------------------------------------------------------------------------------------ channel, v7
@@ -143,6 +147,23 @@ def test_v6_channel_bias_that_v7_removes(oracle_mod):
     b = _bounds(oracle_mod, (1.0, 1.5, 0.3, 0.3), 1, 10_000_000, True)
     p_dm = 0.3 / (1.0 + 1.5e7 + 0.3 + 3e6)
     assert abs((b[2] - b[1]) / TWO32 - p_dm) <= 2.0**-32
+
+
+@pytest.mark.skipif(shutil.which("hipcc") is None, reason="hipcc absent")
+def test_kernel_header_channel_matches_the_oracle(tmp_path, oracle_mod):
+    """The stepper header's chan_target (ecdna-evo_amd/csrc/ssa_device.hpp, host-callable) with the steppers'
+    propensity sequence, compiled for the host and compared with oracle_channel over 1.7M cases: random rates in
+    the accepted range (and zeros), populations 0 .. 2^32 - 1, and the words either side of every boundary
+    (tests/native/device_math_check.cpp). Guards the kernels' channel arithmetic on a machine without a GPU."""
+    exe = tmp_path / "device_math_check"
+    subprocess.run(["hipcc", "-x", "hip", "--offload-host-only", "-std=c++17", "-O1", "-I",
+                    os.path.join(REPO, "ecdna-evo_amd", "csrc"), os.path.join(REPO, "tests", "native",
+                                                                              "device_math_check.cpp"),
+                    "-L", os.path.join(REPO, "oracle", "_build"), "-lecdna_oracle",
+                    "-Wl,-rpath," + os.path.join(REPO, "oracle", "_build"), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert out.stdout.strip().endswith("mismatches=0")
 
 
 def test_time_step_operands_stay_normal():

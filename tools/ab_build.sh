@@ -13,10 +13,10 @@ mkdir -p "$OUT"
 cd "$TMP/ecdna-evo_amd"
 for f in csrc/*.hip csrc/*.cpp; do
   x=""; [ "${f##*.}" = cpp ] && x="-x hip"
-  /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -ffp-contract=off ${EXTRA:-} $x -c "$f" -o "$TMP/$(basename "$f").o"
+  /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -ffp-contract=off -Werror=uninitialized ${EXTRA:-} $x -c "$f" -o "$TMP/$(basename "$f").o"
 done
 if grep -q ECDNA_ILP_BUILD csrc/ssa_kernels.hip; then  # (refs since the two-schedule build)
-  /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -ffp-contract=off ${EXTRA:-} -DECDNA_ILP_BUILD \
+  /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -ffp-contract=off -Werror=uninitialized ${EXTRA:-} -DECDNA_ILP_BUILD \
     -mllvm -amdgpu-sched-strategy=max-ilp -c csrc/ssa_kernels.hip -o "$TMP/ssa_kernels_ilp.o"
 fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libecdna_ssa.so" "$TMP"/*.o -ldl

@@ -9,6 +9,10 @@
 #     c3s        the C3 fixed-total shards (G = 1, 2, 4, 8; all ranks) with the working tree (tools/c3_strong.py)
 #     c3s_knobs  launch knobs on the C3 fixed-total rank-0 shards (G = 2, 4, 8)
 #     c4s        the eight C4 8-GPU shards one after another (tools/c4_shards.sh)
+#     c4split    the C4 shard split by initial copy number onto two concurrent instances (tools/c4_split.py)
+#     prof_bins, prof_rows   tools/gpu_profile.sh ${TAG}_<store> <store>: bench, rocprofv3 kernel trace, PMC passes
+#     bench_ref  the C3 line under the reference's own draws (--store rows --draws reference)
+#     bench_c2, bench_c4, bench_c5   the other workloads' bench lines
 #   LIBS    prebuilt libraries ecdna-evo_amd/lib_ab/<name>/ (tools/ab_build.sh <ref|WORKTREE> <name>)
 #   TAG     prefix of the outputs under gpurun_out/
 # Usage: STEPS=parity,ab_c3 LIBS="base new" TAG=r05x bash tools/gpu_session.sh
@@ -66,6 +70,20 @@ for l in sys.stdin:
       cat $O ;;
     c4s)
       bash tools/c4_shards.sh | tee gpurun_out/${TAG}_c4_shards.txt ;;
+    c4split)
+      timeout -k 10 600 python3 -u tools/c4_split.py > gpurun_out/${TAG}_c4_split.jsonl 2> gpurun_out/${TAG}_c4_split.err
+      cut -c1-200 gpurun_out/${TAG}_c4_split.jsonl ;;
+    prof_bins|prof_rows)
+      unset ECDNA_SSA_ABI_ANY
+      bash tools/gpu_profile.sh ${TAG}_${step#prof_} ${step#prof_} ;;
+    bench_ref)
+      timeout -k 10 600 python3 bench.py --store rows --draws reference > gpurun_out/${TAG}_bench_ref_c3.json \
+        2> gpurun_out/${TAG}_bench_ref_c3.err
+      cut -c1-300 gpurun_out/${TAG}_bench_ref_c3.json ;;
+    bench_c2|bench_c4|bench_c5)
+      timeout -k 10 900 python3 bench.py --workload ${step#bench_} --steps 2 --warmup 1 > gpurun_out/${TAG}_${step}.json \
+        2> gpurun_out/${TAG}_${step}.err
+      cut -c1-300 gpurun_out/${TAG}_${step}.json ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done

@@ -32,7 +32,7 @@ fn = lib.ecdna_dev_path_stats
 fn.argtypes = [C.POINTER(C.c_ulonglong)]
 ctx = engine.Context(spec)
 buf = (C.c_ulonglong * 8)()
-names = ["wave_iters", "lane_iters", "-", "lemire_reject", "large_pick", "binomial_words", "large_row_update",
+names = ["wave_iters", "lane_iters", "boundary", "lemire_reject", "large_pick", "binomial_words", "large_row_update",
          "capacity_gate"]
 for rep in range(1 if workload == "c5" else 2):
     fn(buf)
@@ -41,6 +41,7 @@ for rep in range(1 if workload == "c5" else 2):
     fn(buf)
     d = {k: int(v) for k, v in zip(names, buf)}
     w = max(d["wave_iters"], 1)
-    frac = {k: round(d[k] / w, 5) for k in names[3:]}
-    print(json.dumps({"ms": ms, **d, "lanes_per_wave_iter": round(d["lane_iters"] / w, 2),
+    frac = {k: round(d[k] / w, 5) for k in names[2:]}
+    ev = int(ctx.download().totals["events"].sum())
+    print(json.dumps({"ms": ms, **d, "events": ev, "lanes_per_wave_iter": round(d["lane_iters"] / w, 2),
                       "fraction_of_wave_iters": frac}), flush=True)
