@@ -97,6 +97,12 @@ WORKLOAD_KMAX = {"c2": 32, "c3": BENCH_BIN_KMAX, "c4": 64, "c5": 64}
 # (four workgroups per CU, one replicate per lane for the whole run on one GPU: 22.6 against 28.8 s); its 8-GPU shards
 # (32,768 replicates, paired lanes) stay at K = 64 (9.9 against 10.9 s), profiles/r04s_c5_kmax.txt
 C5_K32_ABOVE = 131_072
+# C4 shards split by initial copy number (shard.k0_split): the sets of k0 = 128 on a K = 256 context,
+# concurrently with the rest on K = 64, the two persistent grids capped at these workgroup counts. Keyed by the
+# number of GPUs the sweep is spread over (rank-0 shards, same box: whole K = 64 -> split 729 -> 655 ms at 1 GPU,
+# 382 -> 340 at 2, 189 -> 185 at 4; at 8 the eight shards' makespan 123 -> 109 ms; profiles/r05_c4_split.txt)
+C4_SPLIT_K0, C4_SPLIT_KMAX = 128, 256
+C4_SPLIT_CAPS = {1: (512, 512), 2: (512, 512), 4: (384, 512), 8: (320, 640)}
 
 
 def default_kmax(workload: str, n: int) -> int:
@@ -290,6 +296,9 @@ def main():
     ap.add_argument("--total", type=int, default=None,
                     help="rehearsal only: replicates in total for the strong-scaling workloads (c2/c4/c5)")
     ap.add_argument("--max-cells", type=int, default=None, help="rehearsal only: override the workload's cell cap")
+    ap.add_argument("--k0-split", choices=("auto", "off"), default="auto",
+                    help="c4, bin store: run the k0 = 128 sets of the shard on a concurrent K = 256 context where "
+                         "C4_SPLIT_CAPS has the GPU count (auto), or the whole shard on one K = 64 context (off)")
     ap.add_argument("--draws", choices=("philox", "reference"), default="philox",
                     help="reference: the Rust reference's own draws seed for seed (ECDNA_FLAG_REFERENCE_DRAWS, "
                          "DESIGN.md §4.1; row store only): the seed-for-seed mode's throughput, not the metric's")
@@ -340,25 +349,53 @@ def main():
     if refdraws:
         spec = dataclasses.replace(spec, flags=spec.flags | abi.FLAG_REFERENCE_DRAWS, _keep=[])
     n_sets = len(spec.rates)
-    ctx = engine.Context(spec)
+    split_caps = C4_SPLIT_CAPS.get(n_gpus) if (args.workload == "c4" and args.k0_split == "auto" and
+                                               args.store == "bins" and args.bin_kmax is None) else None
+    parts = shard.k0_split(spec, C4_SPLIT_K0, C4_SPLIT_KMAX, split_caps) if split_caps else [(spec, 0)]
+    ctxs = [engine.Context(sp) for sp, _ in parts]
+    ctx = ctxs[0]
     hist = torch.zeros(n_sets * spec.hist_bins, dtype=torch.int64, device="cuda")
     tot = torch.zeros(n_sets * 16, dtype=torch.int64, device="cuda")
-    ctx.set_outputs(hist.data_ptr(), tot.data_ptr())
+    part_out = []
+    if len(ctxs) == 1:
+        ctx.set_outputs(hist.data_ptr(), tot.data_ptr())
+    else:  # each part writes its own outputs; the step sums them
+        for c in ctxs:
+            h_p, t_p = torch.zeros_like(hist), torch.zeros_like(tot)
+            c.set_outputs(h_p.data_ptr(), t_p.data_ptr())
+            part_out.append((h_p, t_p))
     torch_stream = torch.cuda.Stream()
     torch.cuda.set_stream(torch_stream)  # torch ops and the engine's kernels share this stream
     stream = torch_stream.cuda_stream
+    part_streams = [torch.cuda.Stream() for _ in ctxs] if len(ctxs) > 1 else []
 
     tot_local = torch.zeros_like(tot)
 
     def step():
-        ctx.launch(stream)
+        if len(ctxs) == 1:
+            ctx.launch(stream)
+        else:  # the parts run concurrently, each on its own stream, joined on the step's stream
+            start = torch.cuda.Event()
+            start.record(torch_stream)
+            for c, s in zip(ctxs, part_streams):
+                s.wait_event(start)
+                c.launch(s.cuda_stream)
+            for s in part_streams:
+                torch_stream.wait_stream(s)
+            torch.add(part_out[0][0], part_out[1][0], out=hist)
+            torch.add(part_out[0][1], part_out[1][1], out=tot)
         tot_local.copy_(tot)  # this GPU's totals, before the reduction
         if distributed:
             shard.reduce_outputs(hist, tot)
 
+    def sync_all():
+        """(stepper ms, histogram ms) of the step: the parts' longest (they run concurrently)"""
+        ms = [c.sync() for c in ctxs]
+        return max(m[0] for m in ms), max(m[1] for m in ms)
+
     for _ in range(args.warmup):
         step()
-        ctx.sync()
+        sync_all()
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -367,7 +404,7 @@ def main():
     kernel_ms, hist_ms = [], []
     for _ in range(args.steps):
         step()
-        s_ms, h_ms = ctx.sync()
+        s_ms, h_ms = sync_all()
         kernel_ms.append(s_ms)
         hist_ms.append(h_ms)
     torch.cuda.synchronize()
@@ -444,8 +481,8 @@ def main():
             # every usable core, as the reference's rayon pool (src/main.rs:221-224)
             threads = int(os.environ.get("ECDNA_BENCH_CPU_THREADS", "0")) or usable_cores()
             cpu = cpu_baseline(threads, args.workload)
-        chunk, lanes = ctx.geometry()
-        instance = ctx.instance()  # the kernel instance timed (auto rules of ecdna_ssa_ctx_create, ABI v7)
+        lanes = sum(c.geometry()[1] for c in ctxs)
+        instance = ctx.instance()  # the kernel instance timed (auto rules of ecdna_ssa_ctx_create)
         line = {
             "metric": METRIC if args.workload == "c3" else f"Gillespie reaction-events/sec, {args.workload.upper()}",
             "value": events_per_step * args.steps / elapsed,
@@ -457,11 +494,11 @@ def main():
             "higher_is_better": True,
             "scaling": "weak" if weak else "strong",
             "vs_baseline": None,
-            # integer cell/counter work plus f32 propensities, channel and time step (draw mapping v6, the reference's
-            # own precision, src/main.rs:67, 139); the engine's clock accumulates in f64
-            "dtype": "u16+f32" if refdraws else "u16+f32 (f64 clock)",
+            # integer cell/counter work plus the reference's f32 propensities (src/main.rs:67, 139) and f32 time step;
+            # the channel's cumulative sums and the engine's clock in f64 (draw mapping v7)
+            "dtype": "u16+f32" if refdraws else "u16+f32 (f64 channel sums and clock)",
             "draws": "reference (ChaCha8 seed*10+i, first-reaction, BINV/BTPE, f32 time; seed for seed)"
-                     if refdraws else "philox (the engine's draw mapping v6, DESIGN.md §3)",
+                     if refdraws else "philox (the engine's draw mapping v7, DESIGN.md §3)",
             "store": args.store,
             "data": "synthetic",
             "config": {
@@ -479,6 +516,11 @@ def main():
                                f"1 RCCL all-reduce of the histogram)",
                 "grid_lanes": lanes,
                 "instance": instance,
+                "k0_split": None if len(ctxs) == 1 else {
+                    "parts": [{"replicates": sp.n_replicates, "bin_kmax": sp.bin_kmax, "max_workgroups": sp.max_workgroups,
+                               "instance": c.instance()} for (sp, _), c in zip(parts, ctxs)],
+                    "note": f"the shard's k0 >= {C4_SPLIT_K0} sets on a K = {C4_SPLIT_KMAX} context, concurrently with "
+                            "the rest (shard.k0_split, DESIGN.md §7); kernel_ms_avg is the longer part's"},
                 "kernel_ms_avg": avg_kernel_s * 1e3,
                 "hist_kernel_ms_avg": sum(hist_ms) / len(hist_ms),
                 "kernel_events_per_s_per_gpu": kernel_eps,
@@ -509,7 +551,8 @@ def main():
             "cpu_baseline": cpu,
         }
         os.write(json_fd, (json.dumps(line) + "\n").encode())
-    ctx.close()
+    for c in ctxs:
+        c.close()
     if distributed:
         dist.destroy_process_group()
 

@@ -69,6 +69,7 @@ int validate(const ecdna_ssa_params_t* p) {
                 return fail(ECDNA_E_INVALID, "rates must be 0 or in [2^-60, 2^60]");
     }
     if (p->reps_per_set == 0) return fail(ECDNA_E_INVALID, "reps_per_set must be >= 1");
+    if (p->reserved0) return fail(ECDNA_E_INVALID, "reserved0 must be 0");
     if (p->hist_bins < 2 || p->hist_bins > ecdna::kMaxHistBins)
         return fail(ECDNA_E_INVALID, "hist_bins must be in [2, 4096]");
     if ((p->flags & ECDNA_FLAG_REP_STATS) && p->hist_bins > 2048)
@@ -587,6 +588,7 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
     if (bpc) per_cu = (int)bpc;
     if (per_cu < 1) per_cu = 1;
     c->stepper_blocks_cap = (uint32_t)(per_cu * c->cus);
+    if (p->max_workgroups) c->stepper_blocks_cap = std::min(c->stepper_blocks_cap, p->max_workgroups);
     uint64_t max_blocks = env_u64("ECDNA_SSA_MAX_BLOCKS", 0);  // testing: force lane refill
     if (max_blocks) c->stepper_blocks_cap = (uint32_t)std::min<uint64_t>(c->stepper_blocks_cap, max_blocks);
 

@@ -14,7 +14,7 @@ from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 # ecdna_process_t (ProcessType, src/clap_app.rs:311-315)
 PURE_BIRTH = 0
@@ -88,6 +88,8 @@ class Params(C.Structure):
         ("replicate_stride", C.c_uint32),
         ("stats_target_hist", C.POINTER(C.c_uint64)),
         ("set_cost_hint", C.POINTER(C.c_float)),
+        ("max_workgroups", C.c_uint32),
+        ("reserved0", C.c_uint32),
     ]
 
 
@@ -215,6 +217,7 @@ class RunSpec:
     bin_kmax: int = 0  # FLAG_BIN_STORE: binned copy numbers 1..bin_kmax (0 = 64)
     set_cost_hint: Optional[Sequence[float]] = None  # per set: start costlier sets first (speed only)
     big_cap: int = 0  # FLAG_BIN_STORE: large-k row capacity (cells with k > bin_kmax); 0 = cell_cap
+    max_workgroups: int = 0  # persistent-grid cap (0 = fill the device); for contexts sharing a GPU (speed only)
     _keep: list = field(default_factory=list, repr=False)
 
     def stride(self) -> int:
@@ -283,6 +286,7 @@ class RunSpec:
         p.flags = self.flags
         p.bin_kmax = self.bin_kmax
         p.big_cap = self.big_cap
+        p.max_workgroups = self.max_workgroups
         p.device = self.device
         if self.snapshots:
             snaps = np.asarray(sorted(int(x) for x in self.snapshots), dtype=np.uint64)

@@ -37,6 +37,37 @@ def weak_range(rank: int, per_rank: int) -> Tuple[int, int]:
     return rank * per_rank, per_rank
 
 
+def k0_split(spec, k0_min: int, wide_kmax: int, caps: Tuple[int, int]):
+    """A bin-store shard split by initial copy number ("C4 shard split"): the replicates whose
+    parameter set starts with a cell of k0 >= k0_min copies run on a second context with K = wide_kmax, whose bins
+    keep their cells in LDS (with K = 64 most of them sit in the large-k row in HBM), concurrently with the rest;
+    caps = (max_workgroups of the rest, of the heavy part) so that the two persistent grids share the GPU. The
+    heavy replicates must be a suffix of the shard's local order (the C4 sweep orders its sets by k0). Each
+    replicate's results are those of a run at its part's K (bin_kmax orders the cells, so K is part of the draw
+    mapping). Returns [(spec, local offset)] of the non-empty parts."""
+    import dataclasses
+
+    import numpy as np
+
+    n, first, stride = spec.n_replicates, spec.first_replicate, spec.stride()
+    if spec.init_per_set is None:
+        k0s = [max(spec.init or {1: 1})] * len(spec.rates)
+    else:
+        k0s = [max(d) if d else 0 for d in spec.init_per_set]
+    sets = (first + np.arange(n, dtype=np.int64) * stride) // spec.reps_per_set
+    heavy = np.asarray(k0s)[sets] >= k0_min
+    i0 = int(np.argmax(heavy)) if heavy.any() else n
+    if not np.all(heavy[i0:]):
+        raise ValueError("k0_split: the heavy replicates are not a suffix of the shard")
+    parts = []
+    if i0 > 0:
+        parts.append((dataclasses.replace(spec, n_replicates=i0, max_workgroups=caps[0], _keep=[]), 0))
+    if i0 < n:
+        parts.append((dataclasses.replace(spec, first_replicate=first + i0 * stride, n_replicates=n - i0,
+                                          bin_kmax=wide_kmax, max_workgroups=caps[1], _keep=[]), i0))
+    return parts
+
+
 def reduce_outputs(hist, totals, group=None) -> None:
     """Sum the per-rank copy-number histograms and totals in place (int64 tensors: u64 counts stay
     far below 2^63). The histogram bins and totals words are plain integer sums, so the result is

@@ -43,9 +43,10 @@
 extern "C" {
 #endif
 
-/* ABI v9: draw mapping v7 (the channel from all 32 bits of the event's word over f64 cumulative propensities,
- * DESIGN.md §3): same layout and entry points as v8, results differ from v8 seed for seed. */
-#define ECDNA_SSA_ABI_VERSION 9
+/* ABI v10: ecdna_ssa_params_t.max_workgroups (a cap on the persistent grid, for contexts that share a GPU
+ * concurrently) appended; draw mapping v7 as in v9 (the channel from all 32 bits of the event's word over f64
+ * cumulative propensities; results differ from v8 seed for seed). */
+#define ECDNA_SSA_ABI_VERSION 10
 
 /* Process type — ProcessType (src/clap_app.rs:311-315); chosen as BirthDeath
  * when d0 > 0 or d1 > 0 (src/clap_app.rs:163-174, 194-200). */
@@ -191,6 +192,12 @@ typedef struct {
      * in id order), which shortens the tail of a run whose sets differ in cost, such as an ABC sweep.
      * Results do not depend on it. NULL: replicates start in id order. */
     const float* set_cost_hint;
+    /* Persistent-grid cap (since ABI v10): at most this many workgroups (0 = as many as the kernel's occupancy
+     * fits on the device). Two contexts launched on two streams of one GPU share its CUs only when their grids
+     * leave room for each other, e.g. a shard split by initial copy number onto two bin-store instances
+     * (DESIGN.md §7). Results do not depend on it. */
+    uint32_t max_workgroups;
+    uint32_t reserved0;             /* must be 0 */
 } ecdna_ssa_params_t;
 
 /* Per-replicate summary statistics of the final distribution (cells = n- + n+, copy number k per cell,

@@ -86,6 +86,44 @@ def test_c4_bench_shard_instance_bit_exact(engine_mod, oracle_mod):
 
 
 @pytest.mark.gpu
+def test_c4_bench_shard_k0_split_bit_exact(engine_mod, oracle_mod):
+    """C4 8-GPU rank-5 shard split as bench.py runs it (C4_SPLIT_CAPS[8]): the k0 = 128 sets' 65,536 replicates on a
+    K = 256 context and the other 458,752 on K = 64, both launched concurrently on two streams with capped grids.
+    Every replicate finishes without error; samples of set 1001 (heavy part, K = 256: its cells stay binned) and set
+    200 (K = 64) equal the oracle at their part's K, and the concurrent run's summaries equal the parts run alone."""
+    import torch
+
+    bench = _bench()
+    first, n, stride = shard.interleaved_range(5, 8, 4_194_304)
+    spec = bench.workload_spec(first, n, 4_194_304, workload="c4", stride=stride)
+    parts = shard.k0_split(spec, bench.C4_SPLIT_K0, bench.C4_SPLIT_KMAX, bench.C4_SPLIT_CAPS[8])
+    assert [(sp.n_replicates, sp.bin_kmax, off) for sp, off in parts] == [(458_752, 64, 0), (65_536, 256, 458_752)]
+    ctxs = [engine_mod.Context(sp) for sp, _ in parts]
+    try:
+        streams = [torch.cuda.Stream() for _ in ctxs]
+        for c, st in zip(ctxs, streams):
+            c.launch(st.cuda_stream)
+        torch.cuda.synchronize()
+        res = []
+        for (sp, _), c in zip(parts, ctxs):
+            c.sync()
+            res.append(c.download())
+            ins = c.instance()  # the grid respects the part's cap
+            assert ins["bin_kmax"] == sp.bin_kmax and ins["grid_lanes"] <= sp.max_workgroups * ins["block_lanes"], ins
+    finally:
+        for c in ctxs:
+            c.close()
+    for r in res:
+        assert np.all(r.summaries["error"] == 0)
+    _compare_sample(res[1], parts[1][0], oracle_mod, (1001 * 4096 - parts[1][0].first_replicate + stride - 1) // stride, 48)
+    _compare_sample(res[0], parts[0][0], oracle_mod, (200 * 4096 - first + stride - 1) // stride, 48)
+    alone = engine_mod.run(parts[1][0])
+    for f in ("nminus", "nplus", "iters", "event_hash"):
+        np.testing.assert_array_equal(alone.summaries[f], res[1].summaries[f], err_msg=f)
+    np.testing.assert_array_equal(alone.summaries["time"].view(np.uint64), res[1].summaries["time"].view(np.uint64))
+
+
+@pytest.mark.gpu
 def test_c4_bench_whole_instance_bit_exact(engine_mod, oracle_mod):
     """C4 on one GPU as `bench.py --workload c4` runs it (4,194,304 replicates, K = 64 / u16, cost-ordered starts,
     16 replicates per lane): the 128-VGPR occupancy build (schedule 2) with the drain control, no rotation (a cost

@@ -2,10 +2,10 @@
 path) run on a wide-K instance (K = 256 by default: their cells stay in LDS bins instead of the large-k
 row) concurrently, on a second stream, with the rest on the K = 64 instance. The shard's interleaved ids (rank r of 8:
 r, r + 8, ...) hit the sets in order, so each class is one contiguous range of local indices and becomes its own
-context (first_replicate, n, stride 8). Each grid is capped (ECDNA_SSA_MAX_BLOCKS, read at create) so that the two
-persistent kernels share the CUs. Prints the makespan (wall time between events around both launches) per setting,
-against the whole shard on one context. Development / measurement tool.
-Usage: [C4S_RANK=0] [C4S_SPLITS=6,7] [C4S_WIDE=256] [C4S_BLOCKS="A:B,..."] python tools/c4_split.py"""
+context (shard.k0_split). Each grid is capped (RunSpec.max_workgroups) so that the two persistent kernels share the
+CUs. Prints the makespan (wall time between events around both launches) per setting, against the whole shard on
+one context. Development / measurement tool.
+Usage: [C4S_RANK=0] [C4S_GPUS=8] [C4S_SPLITS=6,7] [C4S_WIDE=256] [C4S_BLOCKS="A:B,..."] python tools/c4_split.py"""
 import dataclasses
 import json
 import os
@@ -15,19 +15,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import torch  # noqa: E402  (first: one HIP runtime)
 
-from ecdna_evo_amd import abi, engine  # noqa: E402
+from ecdna_evo_amd import abi, engine, shard  # noqa: E402
 import probe_configs  # noqa: E402
-
-
-def ctx_with(spec, max_blocks):
-    if max_blocks:
-        os.environ["ECDNA_SSA_MAX_BLOCKS"] = str(max_blocks)
-    else:
-        os.environ.pop("ECDNA_SSA_MAX_BLOCKS", None)
-    try:
-        return engine.Context(spec)
-    finally:
-        os.environ.pop("ECDNA_SSA_MAX_BLOCKS", None)
 
 
 def timed(ctxs, reps=3):
@@ -54,29 +43,26 @@ def timed(ctxs, reps=3):
 
 def main():
     rank = int(os.environ.get("C4S_RANK", "0"))
+    gpus = int(os.environ.get("C4S_GPUS", "8"))
     wide = int(os.environ.get("C4S_WIDE", "256"))
-    base = dataclasses.replace(probe_configs.c4_shard(rank, 8), flags=abi.FLAG_BIN_STORE, bin_kmax=64, _keep=[])
-    n, first, stride = base.n_replicates, base.first_replicate, base.stride()
-    whole = ctx_with(base, 0)
+    base = dataclasses.replace(probe_configs.c4_shard(rank, gpus), flags=abi.FLAG_BIN_STORE, bin_kmax=64, _keep=[])
+    whole = engine.Context(base)
     ms, per, ev, err = timed([whole])
-    print(json.dumps({"setting": "whole K=64", "makespan_ms": ms, "stepper_ms": per, "events": ev, "errors": err,
-                      "instance": whole.instance()}), flush=True)
+    print(json.dumps({"setting": "whole K=64", "gpus": gpus, "rank": rank, "makespan_ms": ms, "stepper_ms": per,
+                      "events": ev, "errors": err, "instance": whole.instance()}), flush=True)
     whole.close()
-    for ex in [int(x) for x in os.environ.get("C4S_SPLITS", "6,7").split(",")]:
-        s0 = 128 * ex  # first set with k0 = 2^ex (sets are ordered by k0 in blocks of 128)
-        i0 = (4096 * s0 - first + stride - 1) // stride  # first local index in those sets
-        narrow = dataclasses.replace(base, n_replicates=i0, _keep=[])
-        heavy = dataclasses.replace(base, first_replicate=first + i0 * stride, n_replicates=n - i0, bin_kmax=wide,
-                                    _keep=[])
-        for pair in os.environ.get("C4S_BLOCKS", "0:0,512:256,640:128,512:512,384:512").split(","):
-            ba, bb = (int(x) for x in pair.split(":"))
-            ca, cb = ctx_with(narrow, ba), ctx_with(heavy, bb)
-            ms, per, ev, err = timed([ca, cb])
-            print(json.dumps({"setting": f"k0>=2^{ex} on K={wide}", "blocks": [ba, bb], "makespan_ms": ms,
-                              "stepper_ms": per, "replicates": [i0, n - i0], "events": ev, "errors": err,
-                              "grid_lanes": [ca.instance()["grid_lanes"], cb.instance()["grid_lanes"]]}), flush=True)
-            ca.close()
-            cb.close()
+    for ex in [int(x) for x in os.environ.get("C4S_SPLITS", "7").split(",")]:
+        for pair in os.environ.get("C4S_BLOCKS", "320:640,384:512,0:0").split(","):
+            caps = tuple(int(x) for x in pair.split(":"))
+            parts = shard.k0_split(base, 1 << ex, wide, caps)
+            ctxs = [engine.Context(sp) for sp, _ in parts]
+            ms, per, ev, err = timed(ctxs)
+            print(json.dumps({"setting": f"k0>=2^{ex} on K={wide}", "gpus": gpus, "rank": rank, "blocks": list(caps),
+                              "makespan_ms": ms, "stepper_ms": per,
+                              "replicates": [sp.n_replicates for sp, _ in parts], "events": ev, "errors": err,
+                              "grid_lanes": [c.instance()["grid_lanes"] for c in ctxs]}), flush=True)
+            for c in ctxs:
+                c.close()
 
 
 if __name__ == "__main__":
