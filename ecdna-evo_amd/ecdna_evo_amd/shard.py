@@ -54,7 +54,7 @@ def k0_split(spec, k0_min: int, wide_kmax: int, caps: Tuple[int, int]):
         k0s = [max(spec.init or {1: 1})] * len(spec.rates)
     else:
         k0s = [max(d) if d else 0 for d in spec.init_per_set]
-    sets = (first + np.arange(n, dtype=np.int64) * stride) // spec.reps_per_set
+    sets = (first + np.arange(n, dtype=np.int64) * stride) // int(spec.params().reps_per_set)
     heavy = np.asarray(k0s)[sets] >= k0_min
     i0 = int(np.argmax(heavy)) if heavy.any() else n
     if not np.all(heavy[i0:]):

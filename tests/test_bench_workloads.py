@@ -73,3 +73,35 @@ def test_c5_bin_kmax_by_replicates_per_gpu():
     for gpus in (2, 4, 8):
         assert bench.workload_spec(0, total // gpus, total, workload="c5").bin_kmax == 64
     assert bench.workload_spec(0, total, total, workload="c5", bin_kmax=64).bin_kmax == 64
+
+
+@pytest.mark.parametrize("world", sorted(bench.C4_SPLIT_CAPS))
+def test_c4_k0_split_parts_partition_each_shard(world):
+    """shard.k0_split on bench's C4 shards: two parts that together hold the shard's replicates in
+    local order, the second exactly those of the k0 = 128 sets (K = 256), the first the rest (K = 64), each with
+    its workgroup cap from bench.C4_SPLIT_CAPS."""
+    total = bench.WORKLOADS["c4"][0]
+    caps = bench.C4_SPLIT_CAPS[world]
+    for rank in sorted({0, world - 1}):
+        first, n, stride = shard.interleaved_range(rank, world, total)
+        spec = bench.workload_spec(first, n, total, workload="c4", stride=stride)
+        parts = shard.k0_split(spec, bench.C4_SPLIT_K0, bench.C4_SPLIT_KMAX, caps)
+        assert [off for _, off in parts] == [0, parts[0][0].n_replicates]
+        ids = np.concatenate([sp.replicate_ids() for sp, _ in parts])
+        np.testing.assert_array_equal(ids, spec.replicate_ids())
+        (narrow, _), (heavy, _) = parts
+        k0 = np.array([max(d) for d in spec.init_per_set])
+        assert np.all(k0[heavy.replicate_ids() // spec.reps_per_set] == 128)
+        assert np.all(k0[narrow.replicate_ids() // spec.reps_per_set] < 128)
+        assert (narrow.bin_kmax, heavy.bin_kmax) == (64, bench.C4_SPLIT_KMAX)
+        assert (narrow.max_workgroups, heavy.max_workgroups) == caps
+        assert heavy.params().max_workgroups == caps[1] and heavy.params().reserved0 == 0
+
+
+def test_k0_split_refuses_a_shard_whose_heavy_sets_are_not_a_suffix():
+    spec = abi.RunSpec(n_replicates=8, reps_per_set=2, rates=[(1.0, 1.0, 0.0, 0.0)] * 4,
+                       init_per_set=[{1: 1}, {128: 1}, {1: 1}, {128: 1}], flags=abi.FLAG_BIN_STORE, bin_kmax=64)
+    with pytest.raises(ValueError):
+        shard.k0_split(spec, 128, 256, (1, 1))
+    whole = shard.k0_split(abi.RunSpec(n_replicates=4, flags=abi.FLAG_BIN_STORE, bin_kmax=64), 128, 256, (1, 1))
+    assert len(whole) == 1 and whole[0][0].bin_kmax == 64  # no heavy replicate: one part
