@@ -12,6 +12,8 @@
 #     c4split    the C4 shard split by initial copy number onto two concurrent instances (tools/c4_split.py)
 #     prof_bins, prof_rows   tools/gpu_profile.sh ${TAG}_<store> <store>: bench, rocprofv3 kernel trace, PMC passes
 #     bench_ref  the C3 line under the reference's own draws (--store rows --draws reference)
+#     bench_c3, bench_rows   the metric's line (defaults) and the row store's C3 line
+#     smoke      __graft_entry__.smoke()
 #     bench_c2, bench_c4, bench_c5   the other workloads' bench lines
 #   LIBS    prebuilt libraries ecdna-evo_amd/lib_ab/<name>/ (tools/ab_build.sh <ref|WORKTREE> <name>)
 #   TAG     prefix of the outputs under gpurun_out/
@@ -80,6 +82,15 @@ for l in sys.stdin:
       timeout -k 10 600 python3 bench.py --store rows --draws reference > gpurun_out/${TAG}_bench_ref_c3.json \
         2> gpurun_out/${TAG}_bench_ref_c3.err
       cut -c1-300 gpurun_out/${TAG}_bench_ref_c3.json ;;
+    bench_c3)
+      timeout -k 10 600 python3 bench.py > gpurun_out/${TAG}_bench_c3.json 2> gpurun_out/${TAG}_bench_c3.err
+      cut -c1-300 gpurun_out/${TAG}_bench_c3.json ;;
+    bench_rows)
+      timeout -k 10 600 python3 bench.py --store rows > gpurun_out/${TAG}_bench_rows_c3.json 2> gpurun_out/${TAG}_bench_rows_c3.err
+      cut -c1-300 gpurun_out/${TAG}_bench_rows_c3.json ;;
+    smoke)
+      timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.txt 2>&1
+      tail -3 gpurun_out/${TAG}_smoke.txt ;;
     bench_c2|bench_c4|bench_c5)
       timeout -k 10 900 python3 bench.py --workload ${step#bench_} --steps 2 --warmup 1 > gpurun_out/${TAG}_${step}.json \
         2> gpurun_out/${TAG}_${step}.err
