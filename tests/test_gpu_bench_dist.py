@@ -88,8 +88,9 @@ STRONG = {"c4": (1024 * 16, None), "c5": (512, 20_000), "c2": (4096, 2_000)}
 @pytest.mark.parametrize("workload", sorted(STRONG))
 def test_bench_strong_scaling_paths_match_one_process(tmp_path, workload):
     """bench.py --workload c2/c4/c5 under torchrun: one rank over RCCL, and two ranks sharing cuda:0 over gloo
-    (interleaved global-id shards g, g + 2, ...; C4 with its per-set cost hint). The reduced histogram and
-    totals equal one engine run of every id bit for bit, and the line reports strong scaling."""
+    (interleaved global-id shards g, g + 2, ...; C4 with its per-set cost hint and its k0 split). The reduced
+    histogram and totals equal one engine run of every id (C4: of each k0 class at its K) bit for bit, and the line
+    reports strong scaling."""
     total, cells = STRONG[workload]
     extra = ["--workload", workload, "--total", str(total)] + (["--max-cells", str(cells)] if cells else [])
     one = _torchrun(1, 0, tmp_path / "one.npz", {}, extra)
@@ -102,13 +103,21 @@ def test_bench_strong_scaling_paths_match_one_process(tmp_path, workload):
     import bench
     from ecdna_evo_amd import engine
 
-    ctx = engine.Context(bench.workload_spec(0, total, total, workload=workload, max_cells=cells))
-    ctx.launch()
-    ctx.sync()
-    res = ctx.download()
-    ctx.close()
-    ref_hist = res.hist.astype(np.int64).reshape(-1)
-    ref_tot = res.totals.view(np.uint64).astype(np.int64).reshape(-1)
+    from ecdna_evo_amd import shard
+
+    spec = bench.workload_spec(0, total, total, workload=workload, max_cells=cells)
+    # C4: the bench splits every rank's shard by initial copy number (its k0 = 128 replicates on K = 256,
+    # bench.C4_SPLIT_CAPS at 1 and 2 GPUs), so the reference runs the same two classes of ids
+    parts = shard.k0_split(spec, bench.C4_SPLIT_K0, bench.C4_SPLIT_KMAX, (0, 0)) if workload == "c4" else [(spec, 0)]
+    ref_hist, ref_tot = 0, 0
+    for sp, _ in parts:
+        ctx = engine.Context(sp)
+        ctx.launch()
+        ctx.sync()
+        res = ctx.download()
+        ctx.close()
+        ref_hist = ref_hist + res.hist.astype(np.int64).reshape(-1)
+        ref_tot = ref_tot + res.totals.view(np.uint64).astype(np.int64).reshape(-1)
     for f in ("one.npz", "two.npz"):
         d = np.load(tmp_path / f)
         np.testing.assert_array_equal(d["hist"], ref_hist, err_msg=f)
