@@ -763,6 +763,8 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
         hsa.reps_per_set = p.reps_per_set;
         hsa.n = ch.n;
         hsa.bins = p.hist_bins;
+        // (eight workgroups per CU for either histogram pass: one per CU made the bin store's lane-per-replicate
+        // pass no faster at C3, 0.29 -> 0.30 ms, and C4's 1,024 sets 5 -> 28 ms, each workgroup walking more sets)
         const uint32_t hist_blocks_max = (uint32_t)c->cus * 8u;
         uint32_t rpb = (ch.n + hist_blocks_max - 1) / hist_blocks_max;
         if (rpb < 4) rpb = 4;

@@ -19,6 +19,8 @@
 // (the swap_remove pick) plus the row's tail; the tail VALUE is cached in a
 // register (the reference re-reads it through Vec::swap_remove), so a
 // ProliferateNPlus costs one random 2-B load and up to three 2-B stores.
+#include <stdlib.h>
+
 #include "ssa_device.hpp"
 #include "ssa_launch.h"
 
@@ -1783,6 +1785,159 @@ __global__ void __launch_bounds__(kHistBlock) ssa_hist(const HistArgs a) {
     }
 }
 
+// Histogram + totals of the bin store without ABC statistics (the bench's pass). One lane per replicate, 64 at a
+// time per wave: a lane reads its replicate's summary and sums its counters (how many of its N+ cells are binned,
+// so the rest sit at the head of its large-k row), and keeps the totals words in registers; the counters are
+// added to the histogram transposed — lane j holds the running sums of bins j, j + 64, ... over the wave's
+// replicates in registers, read 64 contiguous counters of one replicate per load, 16 replicates' loads in flight —
+// so no two lanes ever add to the same LDS word for them; each lane walks its own replicate's large-k row (up to 64
+// cells; longer ones the whole wave), 8 cells per load. Registers reach the workgroup's LDS histogram once per wave
+// and parameter set. Same sums as ssa_hist<false, BAG>, which walked one replicate per wave: C3 0.64 -> 0.16 ms per
+// launch, C4 (1,024 sets, both parts of the k0 split) 7.7 -> 4.5 ms (profiles/r05s_hist_ab.txt).
+template <int BAG>
+__global__ void __launch_bounds__(kHistBlock) ssa_hist_bags(const HistArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long lds[];
+    unsigned long long* hb = lds;          // [bins]
+    unsigned long long* tb = lds + a.bins;  // [16] totals words
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t nw = blockDim.x >> 6;
+    const uint32_t r_begin = blockIdx.x * a.reps_per_block;
+    if (r_begin >= a.n) return;
+    const uint32_t r_end = min(a.n, r_begin + a.reps_per_block);
+    const uint32_t last = a.bins - 1;
+    const uint32_t bag_k = a.bag_k;  // 32, 64 or 256
+    auto counter = [&](uint64_t q, uint32_t b) -> uint32_t {
+        const uint64_t o = q * bag_k + b;
+        return BAG == 2 ? reinterpret_cast<const uint32_t*>(a.bags)[o]
+                        : (uint32_t)reinterpret_cast<const uint16_t*>(a.bags)[o];
+    };
+
+    uint32_t r = r_begin;
+    while (r < r_end) {
+        const uint64_t set = (a.rid0 + (uint64_t)r * a.rid_stride) / a.reps_per_set;
+        const uint64_t set_end_rid = (set + 1) * a.reps_per_set;
+        const uint64_t in_set = (set_end_rid - a.rid0 + a.rid_stride - 1) / a.rid_stride;
+        const uint32_t seg_end = (uint32_t)min((uint64_t)r_end, in_set);
+        for (uint32_t b = tid; b < a.bins + 16; b += blockDim.x) lds[b] = 0ull;
+        __syncthreads();
+        // totals words 0..8 per lane (replicates, iters, events_by_type[4], uneven, n-, n+); the stop reasons and
+        // errors by ballot (wave-uniform counts)
+        uint64_t t_rep = 0, t_it = 0, t_e0 = 0, t_e1 = 0, t_e2 = 0, t_e3 = 0, t_un = 0, t_nm = 0, t_np = 0;
+        uint32_t t_stop[6] = {0, 0, 0, 0, 0, 0}, t_err = 0;
+        uint64_t acc[4] = {0, 0, 0, 0};  // bins lane + 1, lane + 65, lane + 129, lane + 193
+        for (uint32_t base = r + wave * 64u; base < seg_end; base += nw * 64u) {
+            const uint32_t q = base + lane;
+            const bool valid = q < seg_end;
+            uint32_t nrow = 0, stop = 6u;
+            if (valid) {
+                const ecdna_rep_summary_t* s = a.summaries + q;
+                const uint64_t np = s->nplus;
+                t_rep += 1;
+                t_it += s->iters;
+                t_e0 += s->events_by_type[0];
+                t_e1 += s->events_by_type[1];
+                t_e2 += s->events_by_type[2];
+                t_e3 += s->events_by_type[3];
+                t_un += s->uneven;
+                t_nm += s->nminus;
+                t_np += np;
+                stop = s->stop_reason < 6u ? s->stop_reason : 5u;
+                if (s->error) ++t_err;  // (counted per lane, summed below)
+                // its binned cells: the replicate's counters, 16 B per load (4 u32 or 8 u16 counters)
+                const uint4* v = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.bags) +
+                                                                (uint64_t)q * bag_k * (BAG == 2 ? 4u : 2u));
+                uint32_t small = 0;
+                for (uint32_t b = 0; b < bag_k / (BAG == 2 ? 4u : 8u); ++b) {
+                    const uint4 c = v[b];
+                    if (BAG == 2)
+                        small += c.x + c.y + c.z + c.w;
+                    else
+                        small += (c.x & 0xffffu) + (c.x >> 16) + (c.y & 0xffffu) + (c.y >> 16) + (c.z & 0xffffu) +
+                                 (c.z >> 16) + (c.w & 0xffffu) + (c.w >> 16);
+                }
+                nrow = np >= small ? (uint32_t)(np - small) : 0u;  // (never trust counters past the row)
+            }
+#pragma unroll
+            for (uint32_t st = 0; st < 6u; ++st) t_stop[st] += (uint32_t)__builtin_popcountll(__ballot(stop == st));
+            const uint32_t nq = min(64u, seg_end - base);
+            for (uint32_t i0 = 0; i0 < nq; i0 += 16u) {  // the counters, transposed; 16 loads in flight per lane
+#pragma unroll
+                for (uint32_t m = 0; m < 4u; ++m) {
+                    if (lane + 64u * m >= bag_k) continue;  // (wave-uniform for K = 64, 256)
+                    uint32_t c[16];
+#pragma unroll
+                    for (uint32_t i = 0; i < 16u; ++i) c[i] = i0 + i < nq ? counter(base + i0 + i, lane + 64u * m) : 0u;
+                    uint32_t sum = 0;
+#pragma unroll
+                    for (uint32_t i = 0; i < 16u; ++i) sum += c[i];
+                    acc[m] += sum;
+                }
+            }
+            // the large-k rows: up to 64 cells each lane walks its own replicate's, 8 cells per load; longer rows
+            // (C4's k0 = 128 sets at K = 64) the whole wave, one replicate at a time
+            auto add_cells = [&](uint4 v, uint32_t n_valid) {
+                const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (uint32_t j = 0; j < 8u; ++j) {
+                    if (j < n_valid) {
+                        const uint32_t kk = (wv[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
+                        atomicAdd(&hb[kk < last ? kk : last], 1ull);
+                    }
+                }
+            };
+            const bool long_row = nrow > 64u;
+            const uint16_t* row = a.rows + (uint64_t)q * a.row_stride;
+            for (uint32_t c = 0; c < (long_row ? 0u : nrow); c += 8u)
+                add_cells(*reinterpret_cast<const uint4*>(row + c), nrow - c);
+            uint64_t big = __ballot(long_row);
+            while (big) {
+                const uint32_t i = (uint32_t)__builtin_ctzll(big);
+                big &= big - 1ull;
+                const uint32_t n_i = (uint32_t)__builtin_amdgcn_readlane((int)nrow, (int)i);
+                const uint16_t* row_i = a.rows + (uint64_t)(base + i) * a.row_stride;
+                for (uint32_t c = lane * 8u; c < n_i; c += 512u) add_cells(*reinterpret_cast<const uint4*>(row_i + c), n_i - c);
+            }
+        }
+#pragma unroll
+        for (uint32_t m = 0; m < 4u; ++m) {
+            const uint32_t kk = lane + 64u * m + 1u;
+            if (lane + 64u * m < bag_k && acc[m]) atomicAdd(&hb[kk < last ? kk : last], (unsigned long long)acc[m]);
+        }
+        t_rep = wave_sum(t_rep);
+        t_it = wave_sum(t_it);
+        t_e0 = wave_sum(t_e0);
+        t_e1 = wave_sum(t_e1);
+        t_e2 = wave_sum(t_e2);
+        t_e3 = wave_sum(t_e3);
+        t_un = wave_sum(t_un);
+        t_nm = wave_sum(t_nm);
+        t_np = wave_sum(t_np);
+        t_err = wave_sum(t_err);
+        if (lane == 0 && t_rep) {
+            atomicAdd(&hb[0], (unsigned long long)t_nm);
+            atomicAdd(&tb[0], (unsigned long long)t_rep);
+            atomicAdd(&tb[1], (unsigned long long)t_it);
+            atomicAdd(&tb[2], (unsigned long long)t_e0);
+            atomicAdd(&tb[3], (unsigned long long)t_e1);
+            atomicAdd(&tb[4], (unsigned long long)t_e2);
+            atomicAdd(&tb[5], (unsigned long long)t_e3);
+            atomicAdd(&tb[6], (unsigned long long)t_un);
+            atomicAdd(&tb[7], (unsigned long long)t_nm);
+            atomicAdd(&tb[8], (unsigned long long)t_np);
+#pragma unroll
+            for (uint32_t st = 0; st < 6u; ++st)
+                if (t_stop[st]) atomicAdd(&tb[9 + st], (unsigned long long)t_stop[st]);
+            if (t_err) atomicAdd(&tb[15], (unsigned long long)t_err);
+        }
+        __syncthreads();
+        for (uint32_t b = tid; b < a.bins; b += blockDim.x)
+            if (hb[b]) atomicAdd((unsigned long long*)&a.hist[set * a.bins + b], hb[b]);
+        if (tid < 16 && tb[tid]) atomicAdd(&a.totals[set * 16 + tid], tb[tid]);
+        __syncthreads();
+        r = seg_end;
+    }
+}
+
 // ---------------------------------------------------------------- launch
 
 #ifndef ECDNA_ILP_BUILD
@@ -1897,10 +2052,20 @@ hipError_t launch_hist(const HistArgs& a, uint32_t blocks, hipStream_t stream) {
     void* args[] = {&copy};
     size_t lds = (size_t)(a.bins + 16) * sizeof(unsigned long long);
     if (a.stats) lds += (size_t)(kHistBlock / 64) * a.bins * sizeof(uint32_t);  // per-wave replicate histograms
+    // (the bin store without statistics: one lane per replicate, ssa_hist_bags; ECDNA_HIST_PER_WAVE=1 keeps the
+    // one-replicate-per-wave pass for A/B)
     static const void* const table[2][3] = {
-        {(const void*)ssa_hist<false, 0>, (const void*)ssa_hist<false, 1>, (const void*)ssa_hist<false, 2>},
+        {(const void*)ssa_hist<false, 0>, (const void*)ssa_hist_bags<1>, (const void*)ssa_hist_bags<2>},
         {(const void*)ssa_hist<true, 0>, (const void*)ssa_hist<true, 1>, (const void*)ssa_hist<true, 2>}};
+    static const void* const per_wave[3] = {(const void*)ssa_hist<false, 0>, (const void*)ssa_hist<false, 1>,
+                                            (const void*)ssa_hist<false, 2>};
     const int bag = a.bags ? (a.bag_c32 ? 2 : 1) : 0;
+    static const bool keep_per_wave = [] {
+        const char* e = getenv("ECDNA_HIST_PER_WAVE");
+        return e && e[0] == '1';
+    }();
+    if (keep_per_wave && !a.stats)
+        return hipLaunchKernel(per_wave[bag], dim3(blocks), dim3(kHistBlock), args, lds, stream);
     return hipLaunchKernel(table[a.stats ? 1 : 0][bag], dim3(blocks), dim3(kHistBlock), args, lds, stream);
 }
 #endif  // ECDNA_ILP_BUILD
