@@ -251,6 +251,24 @@ uint64_t env_u64(const char* name, uint64_t dflt) {
     return std::strtoull(v, nullptr, 10);
 }
 
+// The bin stepper's instruction-schedule rule, a pure function of the run's shape and the kernels'
+// occupancies so that the CPU tests can walk any shape through it (ecdna_dev_bin_schedule, tests/test_host.py).
+// Returns ecdna_ssa_instance_t.schedule: 0 occupancy-first, 1 max-ILP, 2 the 128-VGPR build (K = 64 / u16), 3 max-ILP
+// paired lanes, 4 max-ILP lane quads. pair_ok: birth-death without snapshots and a paired instance exists; pair_mode
+// ECDNA_SSA_PAIR (0 off, 1 pairs whenever possible, 2 auto, 3 quads); sched ECDNA_SSA_SCHED (0, 1, 2 auto, 3);
+// max_chunk the largest chunk's replicates; occ_def / occ_ilp workgroups per CU of the two builds.
+int bin_schedule_rule(bool pair_ok, uint64_t pair_mode, uint64_t sched, uint64_t max_chunk, uint32_t cus, bool k64u16,
+                      bool tf0, int occ_def, int occ_ilp, uint32_t stepper_block) {
+    if (pair_ok && pair_mode == 3) return 4;
+    if (pair_ok && (pair_mode == 1 ||
+                    (pair_mode == 2 && sched == 2 && max_chunk <= (uint64_t)cus * (ecdna::kStepperBlock / 2))))
+        return 3;
+    if (sched == 1 || (sched == 2 && max_chunk <= (uint64_t)cus * 256u)) return 1;
+    if (k64u16 && (sched == 3 || (sched == 2 && tf0 && max_chunk >= 4ull * cus * 4u * ecdna::kStepperBlock))) return 2;
+    if (sched == 2 && (occ_ilp >= occ_def || max_chunk < 4ull * (uint64_t)occ_def * cus * stepper_block)) return 1;
+    return 0;
+}
+
 void free_ctx(ecdna_ssa_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
@@ -306,6 +324,13 @@ __attribute__((visibility("hidden"))) int ecdna_ssa_internal_ctx_outputs(ecdna_s
 extern "C" {
 
 int ecdna_ssa_abi_version(void) { return ECDNA_SSA_ABI_VERSION; }
+
+// (development / test entry point, not part of include/ecdna_ssa.h: bin_schedule_rule for the CPU tests)
+int ecdna_dev_bin_schedule(int pair_ok, uint64_t pair_mode, uint64_t sched, uint64_t max_chunk, uint32_t cus,
+                           int k64u16, int tf0, int occ_def, int occ_ilp, uint32_t stepper_block) {
+    return bin_schedule_rule(pair_ok != 0, pair_mode, sched, max_chunk, cus, k64u16 != 0, tf0 != 0, occ_def, occ_ilp,
+                             stepper_block);
+}
 
 const char* ecdna_ssa_strerror(int code) {
     switch (code) {
@@ -558,19 +583,8 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
         const uint64_t pair_mode = env_u64("ECDNA_SSA_PAIR", 2);
         const bool pair_ok = p->process == ECDNA_BIRTH_DEATH && p->n_snapshots == 0 &&
                              ecdna::bin_stepper_kernel_pair(p->segregation, c->bin_k, c->bin_c32, kflags, 2) != nullptr;
-        if (pair_ok && pair_mode == 3)
-            c->bin_ilp = 4;
-        else if (pair_ok && (pair_mode == 1 ||
-                             (pair_mode == 2 && sched == 2 && max_chunk <= (uint64_t)c->cus * (ecdna::kStepperBlock / 2))))
-            c->bin_ilp = 3;
-        else if (sched == 1 || (sched == 2 && max_chunk <= (uint64_t)c->cus * 256u))
-            c->bin_ilp = 1;
-        else if (k64u16 && (sched == 3 || (sched == 2 && tf0 && max_chunk >= 4ull * c->cus * 4u * ecdna::kStepperBlock)))
-            c->bin_ilp = 2;
-        else if (sched == 2 && (occ_ilp >= occ_def || max_chunk < 4ull * (uint64_t)occ_def * c->cus * c->stepper_block))
-            c->bin_ilp = 1;
-        else
-            c->bin_ilp = 0;
+        c->bin_ilp = bin_schedule_rule(pair_ok, pair_mode, sched, max_chunk, c->cus, k64u16, tf0, occ_def, occ_ilp,
+                                       c->stepper_block);
         // bin store: LDS-resident events, bounded by issue and LDS latency: every resident block helps
         CTX_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &per_cu,
