@@ -20,17 +20,17 @@ import sys
 # before the loop (540-860: rotation claims, bin counters, bin search, bags) say nothing about the call site and are
 # left out of the classification
 REGIONS = [
-    (861, 875, "loop top"), (876, 910, "rotation tick"), (911, 916, "loop top"), (917, 1087, "replicate boundary"),
-    (1088, 1088, "loop top"), (1089, 1096, "fast-forward entry test"), (1097, 1360, "N- fast-forward"),
-    (1361, 1382, "propensities and stop tests"), (1383, 1405, "replicate stop"), (1406, 1420, "channel"),
-    (1421, 1434, "word stream setup"), (1435, 1470, "pick"), (1471, 1477, "Lemire rejection"),
-    (1478, 1481, "large-k pick"), (1482, 1513, "segregation"), (1514, 1517, "binomial words"),
-    (1518, 1538, "segregation"), (1539, 1550, "commit"), (1551, 1558, "capacity checks"),
-    (1559, 1574, "bin counter updates"), (1575, 1575, "commit"), (1576, 1599, "large-k row update"),
-    (1600, 1618, "commit (spares, n-, time, hash)"),
+    (863, 877, "loop top"), (878, 912, "rotation tick"), (913, 918, "loop top"), (919, 1089, "replicate boundary"),
+    (1090, 1090, "loop top"), (1091, 1098, "fast-forward entry test"), (1099, 1362, "N- fast-forward"),
+    (1363, 1384, "propensities and stop tests"), (1385, 1407, "replicate stop"), (1408, 1422, "channel"),
+    (1423, 1436, "word stream setup"), (1437, 1472, "pick"), (1473, 1479, "Lemire rejection"),
+    (1480, 1483, "large-k pick"), (1484, 1515, "segregation"), (1516, 1519, "binomial words"),
+    (1520, 1540, "segregation"), (1541, 1552, "commit"), (1553, 1560, "capacity checks"),
+    (1561, 1576, "bin counter updates"), (1577, 1577, "commit"), (1578, 1601, "large-k row update"),
+    (1602, 1620, "commit (spares, n-, time, hash)"),
 ]
-HELPERS = [(540, 660, "rotation claims"), (682, 727, "bin counter updates"), (732, 775, "bin search"),
-           (776, 860, "bins, bags")]
+HELPERS = [(542, 662, "rotation claims"), (684, 729, "bin counter updates"), (734, 777, "bin search"),
+           (778, 862, "bins, bags")]
 # ssa_device.hpp functions (line ranges)
 DEVICE = [
     (27, 117, "Philox block"), (118, 143, "soft log"), (144, 160, "channel"), (161, 173, "time step (division)"),
@@ -98,7 +98,7 @@ def main(path, sym, stats_line, pmc_line):
     blocks = parse(path, sym)
     # the event loop: the loop the propensity block sits in
     main_hdr = next(b["loop"][0] for b in blocks
-                    if b["loop"] and any(f.endswith("ssa_kernels.hip") and 1366 <= ln <= 1382 for (_, f, ln) in b["ins"]))
+                    if b["loop"] and any(f.endswith("ssa_kernels.hip") and 1368 <= ln <= 1384 for (_, f, ln) in b["ins"]))
 
     def own_class(ins):
         """class from a set of instructions' lines: the binomial's device code, else the majority event-loop region"""
