@@ -99,10 +99,10 @@ WORKLOAD_KMAX = {"c2": 32, "c3": BENCH_BIN_KMAX, "c4": 64, "c5": 64}
 C5_K32_ABOVE = 131_072
 # C4 shards split by initial copy number (shard.k0_split): the sets of k0 = 128 on a K = 256 context,
 # concurrently with the rest on K = 64, the two persistent grids capped at these workgroup counts. Keyed by the
-# number of GPUs the sweep is spread over (rank-0 shards, same box: whole K = 64 -> split 729 -> 655 ms at 1 GPU,
-# 382 -> 340 at 2, 189 -> 185 at 4; at 8 the eight shards' makespan 123 -> 109 ms; profiles/r05_c4_split.txt)
+# number of GPUs the sweep is spread over (rank-0 shards, same box: whole K = 64 -> split 727 -> 638 ms at 1 GPU,
+# 372 -> 322 at 2, 189 -> 185 at 4; at 8 the eight shards' makespan 124 -> 108 ms; profiles/r05_c4_split.txt)
 C4_SPLIT_K0, C4_SPLIT_KMAX = 128, 256
-C4_SPLIT_CAPS = {1: (512, 512), 2: (512, 512), 4: (384, 512), 8: (320, 640)}
+C4_SPLIT_CAPS = {1: (496, 528), 2: (496, 528), 4: (384, 512), 8: (336, 624)}
 
 
 def default_kmax(workload: str, n: int) -> int:
