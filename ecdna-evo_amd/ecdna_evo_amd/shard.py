@@ -50,6 +50,8 @@ def k0_split(spec, k0_min: int, wide_kmax: int, caps: Tuple[int, int]):
     import numpy as np
 
     n, first, stride = spec.n_replicates, spec.first_replicate, spec.stride()
+    if n == 0:
+        return [(spec, 0)]
     if spec.init_per_set is None:
         k0s = [max(spec.init or {1: 1})] * len(spec.rates)
     else:

@@ -105,3 +105,5 @@ def test_k0_split_refuses_a_shard_whose_heavy_sets_are_not_a_suffix():
         shard.k0_split(spec, 128, 256, (1, 1))
     whole = shard.k0_split(abi.RunSpec(n_replicates=4, flags=abi.FLAG_BIN_STORE, bin_kmax=64), 128, 256, (1, 1))
     assert len(whole) == 1 and whole[0][0].bin_kmax == 64  # no heavy replicate: one part
+    empty = shard.k0_split(abi.RunSpec(n_replicates=0, flags=abi.FLAG_BIN_STORE, bin_kmax=64), 1, 256, (1, 1))
+    assert len(empty) == 1 and empty[0][0].n_replicates == 0  # (an empty shard stays one context)
