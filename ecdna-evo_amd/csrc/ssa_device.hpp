@@ -59,20 +59,27 @@ __device__ __forceinline__ PhiloxKeys philox_round_keys(uint32_t k0, uint32_t k1
     return r;
 }
 
-// a ^ b ^ c as one gfx950 v_bitop3_b32 (truth table 0x96) instead of two v_xor_b32
+// a ^ b ^ c as one gfx950 v_bitop3_b32 (truth table 0x96) instead of two v_xor_b32. B3: the compiler builtin, whose
+// hazards the compiler sees (an inline asm block is opaque: each is followed by a conservative s_nop before the next
+// v_mad_u64_u32, and the scheduler works around it). Same instruction, same result; only the schedule differs: the
+// builtin is faster where waves drain or run alone (C4 shard -4 %, C5 shard -2 %) and 1 % slower on the issue-bound
+// C3 kernel (profiles/r05zb_bitop3_ab.txt), so the bin stepper picks it per instance (kB3).
+template <bool B3 = false>
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    if (B3) return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
     uint32_t d;
     asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
     return d;
 }
 
+template <bool B3 = false>
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, const PhiloxKeys& rk) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         const uint64_t p0 = (uint64_t)kPhiloxM0 * c.x;
         const uint64_t p1 = (uint64_t)kPhiloxM1 * c.z;
-        c = make_uint4(xor3((uint32_t)(p1 >> 32), c.y, rk.k0[r]), (uint32_t)p1,
-                       xor3((uint32_t)(p0 >> 32), c.w, rk.k1[r]), (uint32_t)p0);
+        c = make_uint4(xor3<B3>((uint32_t)(p1 >> 32), c.y, rk.k0[r]), (uint32_t)p1,
+                       xor3<B3>((uint32_t)(p0 >> 32), c.w, rk.k1[r]), (uint32_t)p0);
     }
     return c;
 }
@@ -93,6 +100,7 @@ __device__ __forceinline__ PhiloxEventPre philox_event_pre(uint32_t rid_lo, uint
 }
 
 // == philox4x32_10(make_uint4(e, 0, rid_lo, rid_hi), rk) for the pre formed from (rid_lo, rid_hi)
+template <bool B3 = false>
 __device__ __forceinline__ uint4 philox_event(uint32_t e, const PhiloxEventPre& pre, const PhiloxKeys& rk) {
     const uint64_t p0 = (uint64_t)kPhiloxM0 * e;
     uint4 c = make_uint4(pre.x0, pre.x1, (uint32_t)(p0 >> 32) ^ pre.x2, (uint32_t)p0);
@@ -100,8 +108,8 @@ __device__ __forceinline__ uint4 philox_event(uint32_t e, const PhiloxEventPre& 
     for (int r = 1; r < 10; ++r) {
         const uint64_t q0 = (uint64_t)kPhiloxM0 * c.x;
         const uint64_t q1 = (uint64_t)kPhiloxM1 * c.z;
-        c = make_uint4(xor3((uint32_t)(q1 >> 32), c.y, rk.k0[r]), (uint32_t)q1,
-                       xor3((uint32_t)(q0 >> 32), c.w, rk.k1[r]), (uint32_t)q0);
+        c = make_uint4(xor3<B3>((uint32_t)(q1 >> 32), c.y, rk.k0[r]), (uint32_t)q1,
+                       xor3<B3>((uint32_t)(q0 >> 32), c.w, rk.k1[r]), (uint32_t)q0);
     }
     return c;
 }
@@ -325,9 +333,10 @@ struct WordStream {
         return redraw_even_small_with(n, tries, max_tries, fail, [&](uint4 c4) { return philox4x32_10(c4, k0, k1); });
     }
 
+    template <bool B3 = false>
     __device__ __forceinline__ uint32_t redraw_even_small(uint32_t n, uint32_t tries, uint32_t max_tries, bool& fail,
                                                           const PhiloxKeys& rk) {
-        return redraw_even_small_with(n, tries, max_tries, fail, [&](uint4 c4) { return philox4x32_10(c4, rk); });
+        return redraw_even_small_with(n, tries, max_tries, fail, [&](uint4 c4) { return philox4x32_10<B3>(c4, rk); });
     }
 
     // with the key schedule formed per block (k0, k1)
@@ -338,9 +347,9 @@ struct WordStream {
     // with the kernel's VGPR round keys. (A reference, never a nullable pointer: a null test of the keys'
     // private-memory address does not fold on AMDGPU, where private null is not address 0, and the test alone
     // kept the 20 keys in scratch, reloaded at every Philox round of every kernel that had it.)
-    template <bool kReuse = false>
+    template <bool kReuse = false, bool B3 = false>
     __device__ __forceinline__ uint32_t binomial_half(uint32_t n, const PhiloxKeys& rk) {
-        return binomial_half_with<kReuse>(n, [&](uint4 c4) { return philox4x32_10(c4, rk); });
+        return binomial_half_with<kReuse>(n, [&](uint4 c4) { return philox4x32_10<B3>(c4, rk); });
     }
 };
 

@@ -658,6 +658,9 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
     const uint32_t tid = threadIdx.x;
     const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
     const PhiloxKeys rk = philox_round_keys(k0, k1);  // event blocks: round keys in VGPRs
+    // the Philox blocks' XOR3 as the compiler builtin (ssa_device.hpp xor3) in the K = 64 / 256 and paired instances
+    // (C4, C5 shards: waves that drain or run alone); the issue-bound K = 32 kernel (C3) keeps the asm form
+    constexpr bool kB3 = NG >= 8 || PAIR != 0;
     PhiloxEventPre pre{0u, 0u, 0u};  // the replicate-only part of round 0
     PATH_STATS_DECL;
     const uint32_t stop32 = a.stop_cells < 0xffffffffull ? (uint32_t)a.stop_cells : 0xffffffffu;
@@ -1125,7 +1128,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                 // continues advances both by 2 (a lane that commits fewer leaves, and its next words go unused)
                 uint32_t ctr = __builtin_amdgcn_permlane32_swap(e, e, false, false)[0] + 1u;
                 ctr = helper ? ctr : e;
-                uint4 wb = philox_event(ctr, hp, rk);
+                uint4 wb = philox_event<kB3>(ctr, hp, rk);
                 SoftlogParts lp = softlog_begin(wb.x, logtab);  // (finished at the top of the step that uses it)
 #pragma unroll 1
                 for (uint32_t q = 0; q < kFfMax; q += 2) {
@@ -1152,7 +1155,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     const float lga = lg;
                     // the next step's words (events e + 2, e + 3), off this step's chain
                     ctr += 2u;
-                    wb = philox_event(ctr, hp, rk);
+                    wb = philox_event<kB3>(ctr, hp, rk);
                     lp = softlog_begin(wb.x, logtab);
                     // event e (conditions as 0/1 words combined with bitwise ops: no short-circuit branches, so
                     // the step stays one basic block for the scheduler)
@@ -1236,7 +1239,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                 const double qpb = quad_bcast_d<0>(pbf), qpd = quad_bcast_d<0>(pdf);
                 const uint32_t qnpf = quad_bcast<0>(npf);
                 uint32_t ctr = e + qlane;
-                uint4 wb = philox_event(ctr, pre, rk);
+                uint4 wb = philox_event<kB3>(ctr, pre, rk);
                 SoftlogParts lp = softlog_begin(wb.x, logtab);
 #pragma unroll 1
                 for (uint32_t q = 0; q < kFfMaxQuad; q += 4) {
@@ -1247,7 +1250,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     const float lg = softlog_end(lp);  // this lane's event e + qlane
                     const uint4 wa = wb;
                     ctr += 4u;  // the next step's words (events e + 4 + qlane), off this step's chain
-                    wb = philox_event(ctr, pre, rk);
+                    wb = philox_event<kB3>(ctr, pre, rk);
                     lp = softlog_begin(wb.x, logtab);
                     const uint32_t y0 = quad_bcast<0>(wa.y), y1 = quad_bcast<1>(wa.y), y2 = quad_bcast<2>(wa.y),
                                    y3 = quad_bcast<3>(wa.y);
@@ -1336,7 +1339,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                         if ((e >= a.max_iter) || nm + npf >= stop32 || t_over2 || !(a02 > 0.0f)) {
                             go = false;
                         } else {
-                            const uint4 w2 = philox_event(e, pre, rk);
+                            const uint4 w2 = philox_event<kB3>(e, pre, rk);
                             const double target2 = chan_target(w2.y, A2);
                             // the channel as lane masks: ProliferateNMinus !g0, DeathNMinus g1 & !g2
                             const bool g0 = target2 >= cA2, g1 = target2 >= cB2, g2 = target2 >= cC2;
@@ -1407,7 +1410,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
 
             CYC_MARK(8);
             const uint32_t rid_lo = (uint32_t)rid, rid_hi = (uint32_t)(rid >> 32);
-            const uint4 w = philox_event(e, pre, rk);
+            const uint4 w = philox_event<kB3>(e, pre, rk);
             // direct method: the channel is the number of cumulative propensities <= target (the first i
             // with target < c_i; the c_i are non-decreasing); (w1 + 0.5) 2^-32 times A, in f64 (chan_target)
             const double target = chan_target(w.y, A);
@@ -1462,7 +1465,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                         k_ahead = gload_u16_l2(row + (idx - ns));
                         tail_ahead = gload_u16_l2(row + (nb - 1u));
                         if (prolif) {
-                            ws.blk = philox4x32_10(make_uint4(e, 1u, rid_lo, rid_hi), rk);
+                            ws.blk = philox4x32_10<kB3>(make_uint4(e, 1u, rid_lo, rid_hi), rk);
                             ws.blk_id = 1u;
                         }
                     }
@@ -1515,13 +1518,13 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                 if (prolif && fast) ws.pos = fast1 ? 2u : 3u;
                 if (prolif && !fast && k <= 32767u) {  // larger copy numbers or a rejected pick: more words
                     PATH_STAT(5);
-                    k1v = ws.binomial_half<kAhead>(n, rk);
+                    k1v = ws.binomial_half<kAhead, kB3>(n, rk);
                 }
                 if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN && prolif && (k1v == 0u || k1v == n)) {
                     // src/segregation.rs:157-174: redraw while uneven (the first draw above was try 1)
                     if (n <= 32u) {
                         bool fail = false;
-                        k1v = ws.redraw_even_small(n, 1u, kNoUnevenMaxTries, fail, rk);
+                        k1v = ws.redraw_even_small<kB3>(n, 1u, kNoUnevenMaxTries, fail, rk);
                         if (fail) ev_err = ECDNA_REP_ERR_REJECTION;
                     } else {
                         uint32_t tries = 1;
@@ -1530,7 +1533,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                                 ev_err = ECDNA_REP_ERR_REJECTION;
                                 break;
                             }
-                            k1v = ws.binomial_half<kAhead>(n, rk);
+                            k1v = ws.binomial_half<kAhead, kB3>(n, rk);
                             ++tries;
                         }
                     }
