@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build libecdna_ssa.so from the kernel/ABI sources of a git ref into ecdna-evo_amd/lib_ab/<ref>/,
 # for a same-box A/B against the working tree (ECDNA_SSA_LIB=<that path> python tools/sweep.py ...).
-# Usage: [EXTRA=-DFLAG] bash tools/ab_build.sh <git-ref or WORKTREE> [out-name]
+# Usage: [EXTRA=-DFLAG] [ILP_STRATEGY=max-ilp] bash tools/ab_build.sh <git-ref or WORKTREE> [out-name]
 set -euo pipefail
 REF=${1:?git ref}
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -17,7 +17,7 @@ for f in csrc/*.hip csrc/*.cpp; do
 done
 if grep -q ECDNA_ILP_BUILD csrc/ssa_kernels.hip; then  # (refs since the two-schedule build)
   /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -ffp-contract=off -Werror=uninitialized ${EXTRA:-} -DECDNA_ILP_BUILD \
-    -mllvm -amdgpu-sched-strategy=max-ilp -c csrc/ssa_kernels.hip -o "$TMP/ssa_kernels_ilp.o"
+    -mllvm -amdgpu-sched-strategy=${ILP_STRATEGY:-max-ilp} -c csrc/ssa_kernels.hip -o "$TMP/ssa_kernels_ilp.o"
 fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libecdna_ssa.so" "$TMP"/*.o -ldl
 echo "$OUT/libecdna_ssa.so"
