@@ -89,26 +89,32 @@ def valu_measured_ceilings():
 BENCH_BIN_KMAX = 32
 
 
-# bin_kmax per workload (measured): K = 32 where the pick scan dominates (C3 issue-bound: 5 %
-# faster than 64; C2), K = 64 where copy numbers spread (C4: k0 up to 128, 8-GPU makespan 156 -> 131 ms;
-# C5: 1e6 cells)
+# bin_kmax per workload (measured). K is part of the draw mapping (it fixes the canonical cell order,
+# DESIGN.md §3.3), so it is a property of the WORKLOAD, never of the GPU count: the same replicate ids give the same
+# results on 1, 2, ..., 8 GPUs. K = 32 where the pick scan dominates (C3 issue-bound:
+# 5 % faster than 64; C2), K = 64 where copy numbers spread (C4: k0 up to 128, 8-GPU makespan 156 -> 131 ms; C5: 1e6
+# cells). C5 is the 8-GPU config (BASELINE.json configs[4]): its 8-, 4- and 2-GPU shards run faster at K = 64 (9.9
+# against 10.9 s, 13.0 against 14.0, 15.5 against 16.2; profiles/r04s_c5_kmax.txt, r04u_kmax_rule.txt) and the whole
+# run on one GPU slower (28.8 against 22.6 s); until round 5 the one-GPU run took K = 32, which made its results
+# differ from the shards' seed for seed.
 WORKLOAD_KMAX = {"c2": 32, "c3": BENCH_BIN_KMAX, "c4": 64, "c5": 64}
-# C5 holding more replicates on a GPU than K = 64's grid has lanes (131,072: two workgroups per CU, LDS-bound): K = 32
-# (four workgroups per CU, one replicate per lane for the whole run on one GPU: 22.6 against 28.8 s); its 8-GPU shards
-# (32,768 replicates, paired lanes) stay at K = 64 (9.9 against 10.9 s), profiles/r04s_c5_kmax.txt
-C5_K32_ABOVE = 131_072
 # C4 shards split by initial copy number (shard.k0_split): the sets of k0 = 128 on a K = 256 context,
-# concurrently with the rest on K = 64, the two persistent grids capped at these workgroup counts. Keyed by the
-# number of GPUs the sweep is spread over (rank-0 shards, same box: whole K = 64 -> split 727 -> 638 ms at 1 GPU,
-# 372 -> 322 at 2, 189 -> 185 at 4; at 8 the eight shards' makespan 124 -> 108 ms; profiles/r05_c4_split.txt)
+# concurrently with the rest on K = 64, the two persistent grids capped at these workgroup counts. The split is part of
+# the workload (which K a replicate runs at), at every GPU count; the caps are speed only (results never depend on the
+# grid), measured for 1, 2, 4 and 8 GPUs (rank-0 shards, same box: whole K = 64 -> split 727 -> 638 ms at 1 GPU,
+# 372 -> 322 at 2, 189 -> 185 at 4; at 8 the eight shards' makespan 124 -> 108 ms; profiles/r05_c4_split.txt); other
+# counts take those of the nearest measured count below.
 C4_SPLIT_K0, C4_SPLIT_KMAX = 128, 256
 C4_SPLIT_CAPS = {1: (496, 528), 2: (496, 528), 4: (384, 512), 8: (336, 624)}
 
 
-def default_kmax(workload: str, n: int) -> int:
-    """The workload's bin store K for a GPU holding n replicates."""
-    if workload == "c5" and n > C5_K32_ABOVE:
-        return 32
+def c4_split_caps(n_gpus: int):
+    """(narrow, heavy) workgroup caps of the C4 k0 split for a sweep spread over n_gpus GPUs."""
+    return C4_SPLIT_CAPS[max(g for g in C4_SPLIT_CAPS if g <= max(1, n_gpus))]
+
+
+def default_kmax(workload: str, n: int = 0) -> int:
+    """The workload's bin store K (the same for any shard size n: K is part of the draw mapping)."""
     return WORKLOAD_KMAX[workload]
 
 
@@ -237,6 +243,49 @@ def rmw_ceiling():
     return best
 
 
+@dataclasses.dataclass
+class RankParts:
+    weak: bool             # the metric's weak-scaling C3 line
+    c3_strong: bool        # C3's fixed-total reading
+    total: int             # replicates over all ranks
+    reps: int              # replicates on this rank
+    spec: abi.RunSpec      # this rank's shard
+    parts: list            # [(RunSpec, local offset)]: the contexts the rank launches (C4: split by k0)
+
+
+def rank_parts(workload: str, n_gpus: int, rank: int, scaling: str = "weak", store: str = "bins",
+               bin_kmax: Optional[int] = None, k0_split: str = "auto", total: Optional[int] = None,
+               reps_per_gpu: int = REPS_PER_GPU, max_cells: Optional[int] = None, device: int = 0,
+               refdraws: bool = False) -> RankParts:
+    """What rank `rank` of `n_gpus` runs for a workload: its shard of global replicate ids and the engine contexts
+    it launches. Which K (draw mapping) a replicate runs at depends on its id and the workload only,
+    never on n_gpus, so every GPU count gives the same per-replicate results (tests/test_bench_workloads.py)."""
+    weak = workload == "c3" and scaling == "weak"
+    c3_strong = workload == "c3" and scaling == "strong"
+    if weak:  # the metric's line: 2^20 replicates per GPU, rank g owns ids [g 2^20, (g+1) 2^20)
+        reps = reps_per_gpu
+        total = reps * n_gpus
+        first, n = shard.weak_range(rank, reps)
+        stride = 1
+    elif c3_strong:  # the metric's fixed-total reading: 2^20 in total, rank g owns a contiguous 1/N of them
+        total = total or REPS_PER_GPU
+        first, n = shard.shard_range(rank, n_gpus, total)
+        stride = 1
+        reps = n
+    else:  # a fixed total over the ranks, interleaved ids (DESIGN.md §7)
+        total = total or WORKLOADS[workload][0]
+        first, n, stride = shard.interleaved_range(rank, n_gpus, total)
+        reps = n
+    spec = workload_spec(first, n, total, device=device, store=store, bin_kmax=bin_kmax, workload=workload,
+                         stride=stride, max_cells=max_cells)
+    if refdraws:
+        spec = dataclasses.replace(spec, flags=spec.flags | abi.FLAG_REFERENCE_DRAWS, _keep=[])
+    split_caps = c4_split_caps(n_gpus) if (workload == "c4" and k0_split == "auto" and store == "bins" and
+                                           bin_kmax is None) else None
+    parts = shard.k0_split(spec, C4_SPLIT_K0, C4_SPLIT_KMAX, split_caps) if split_caps else [(spec, 0)]
+    return RankParts(weak, c3_strong, total, reps, spec, parts)
+
+
 def cpu_baseline(threads: int, workload: str = "c3"):
     """Reference-semantics CPU path (oracle compat mode) timed on a bounded sample of the workload: its
     first replicates (C4: ids spread evenly over the id range, so the sample spans every set)."""
@@ -297,8 +346,9 @@ def main():
                     help="rehearsal only: replicates in total for the strong-scaling workloads (c2/c4/c5)")
     ap.add_argument("--max-cells", type=int, default=None, help="rehearsal only: override the workload's cell cap")
     ap.add_argument("--k0-split", choices=("auto", "off"), default="auto",
-                    help="c4, bin store: run the k0 = 128 sets of the shard on a concurrent K = 256 context where "
-                         "C4_SPLIT_CAPS has the GPU count (auto), or the whole shard on one K = 64 context (off)")
+                    help="c4, bin store: run the k0 = 128 sets of the shard on a concurrent K = 256 context (auto, any "
+                         "GPU count), or the whole shard on one K = 64 context (off; the k0 = 128 replicates then "
+                         "run at K = 64 and differ seed for seed)")
     ap.add_argument("--draws", choices=("philox", "reference"), default="philox",
                     help="reference: the Rust reference's own draws seed for seed (ECDNA_FLAG_REFERENCE_DRAWS, "
                          "DESIGN.md §4.1; row store only): the seed-for-seed mode's throughput, not the metric's")
@@ -325,33 +375,14 @@ def main():
     n_gpus = world
     if args.scaling == "strong" and args.workload != "c3":
         ap.error("--scaling strong applies to c3 (the other workloads are fixed totals already)")
-    weak = args.workload == "c3" and args.scaling == "weak"
-    c3_strong = args.workload == "c3" and args.scaling == "strong"
-    if weak:  # the metric's line: 2^20 replicates per GPU, rank g owns ids [g 2^20, (g+1) 2^20)
-        reps = args.reps_per_gpu
-        total = reps * n_gpus
-        first, n = shard.weak_range(rank, reps)
-        stride = 1
-    elif c3_strong:  # the metric's fixed-total reading: 2^20 in total, rank g owns a contiguous 1/N of them
-        total = args.total or REPS_PER_GPU
-        first, n = shard.shard_range(rank, n_gpus, total)
-        stride = 1
-        reps = n
-    else:  # a fixed total over the ranks, interleaved ids
-        total = args.total or WORKLOADS[args.workload][0]
-        first, n, stride = shard.interleaved_range(rank, n_gpus, total)
-        reps = n
     refdraws = args.draws == "reference"
     if refdraws and args.store != "rows":
         ap.error("--draws reference runs on the row store only (--store rows)")
-    spec = workload_spec(first, n, total, device=local if distributed else 0, store=args.store,
-                         bin_kmax=args.bin_kmax, workload=args.workload, stride=stride, max_cells=args.max_cells)
-    if refdraws:
-        spec = dataclasses.replace(spec, flags=spec.flags | abi.FLAG_REFERENCE_DRAWS, _keep=[])
+    rp = rank_parts(args.workload, n_gpus, rank, scaling=args.scaling, store=args.store, bin_kmax=args.bin_kmax,
+                    k0_split=args.k0_split, total=args.total, reps_per_gpu=args.reps_per_gpu, max_cells=args.max_cells,
+                    device=local if distributed else 0, refdraws=refdraws)
+    weak, c3_strong, total, reps, spec, parts = rp.weak, rp.c3_strong, rp.total, rp.reps, rp.spec, rp.parts
     n_sets = len(spec.rates)
-    split_caps = C4_SPLIT_CAPS.get(n_gpus) if (args.workload == "c4" and args.k0_split == "auto" and
-                                               args.store == "bins" and args.bin_kmax is None) else None
-    parts = shard.k0_split(spec, C4_SPLIT_K0, C4_SPLIT_KMAX, split_caps) if split_caps else [(spec, 0)]
     ctxs = [engine.Context(sp) for sp, _ in parts]
     ctx = ctxs[0]
     hist = torch.zeros(n_sets * spec.hist_bins, dtype=torch.int64, device="cuda")

@@ -70,6 +70,9 @@ int validate(const ecdna_ssa_params_t* p) {
     }
     if (p->reps_per_set == 0) return fail(ECDNA_E_INVALID, "reps_per_set must be >= 1");
     if (p->reserved0) return fail(ECDNA_E_INVALID, "reserved0 must be 0");
+    // (bit 31 is the library's internal snapshot bit, kFlagSnapshotsRt: a caller setting it, or any other unknown bit,
+    // would silently select another kernel instance)
+    if (p->flags & ~(uint32_t)ECDNA_FLAG_ALL) return fail(ECDNA_E_INVALID, "unknown bits in flags");
     if (p->hist_bins < 2 || p->hist_bins > ecdna::kMaxHistBins)
         return fail(ECDNA_E_INVALID, "hist_bins must be in [2, 4096]");
     if ((p->flags & ECDNA_FLAG_REP_STATS) && p->hist_bins > 2048)
@@ -254,12 +257,11 @@ uint64_t env_u64(const char* name, uint64_t dflt) {
 // The bin stepper's instruction-schedule rule, a pure function of the run's shape and the kernels'
 // occupancies so that the CPU tests can walk any shape through it (ecdna_dev_bin_schedule, tests/test_host.py).
 // Returns ecdna_ssa_instance_t.schedule: 0 occupancy-first, 1 max-ILP, 2 the 128-VGPR build (K = 64 / u16), 3 max-ILP
-// paired lanes, 4 max-ILP lane quads. pair_ok: birth-death without snapshots and a paired instance exists; pair_mode
-// ECDNA_SSA_PAIR (0 off, 1 pairs whenever possible, 2 auto, 3 quads); sched ECDNA_SSA_SCHED (0, 1, 2 auto, 3);
+// paired lanes. pair_ok: birth-death without snapshots and a paired instance exists; pair_mode ECDNA_SSA_PAIR (0 off,
+// 1 pairs whenever possible, 2 auto); sched ECDNA_SSA_SCHED (0, 1, 2 auto, 3);
 // max_chunk the largest chunk's replicates; occ_def / occ_ilp workgroups per CU of the two builds.
 int bin_schedule_rule(bool pair_ok, uint64_t pair_mode, uint64_t sched, uint64_t max_chunk, uint32_t cus, bool k64u16,
                       bool tf0, int occ_def, int occ_ilp, uint32_t stepper_block) {
-    if (pair_ok && pair_mode == 3) return 4;
     if (pair_ok && (pair_mode == 1 ||
                     (pair_mode == 2 && sched == 2 && max_chunk <= (uint64_t)cus * (ecdna::kStepperBlock / 2))))
         return 3;
@@ -579,10 +581,9 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
         // idle half of each wave computes the next event's Philox block and soft log in the N- fast-forward.
         // Birth-death without snapshots (the fast-forward's domain). ECDNA_SSA_PAIR = 0 off, 1 whenever
         // possible, 2 auto.
-        // Quads (ECDNA_SSA_PAIR = 3 whenever possible): four lanes per replicate, four events per fast-forward step.
         const uint64_t pair_mode = env_u64("ECDNA_SSA_PAIR", 2);
         const bool pair_ok = p->process == ECDNA_BIRTH_DEATH && p->n_snapshots == 0 &&
-                             ecdna::bin_stepper_kernel_pair(p->segregation, c->bin_k, c->bin_c32, kflags, 2) != nullptr;
+                             ecdna::bin_stepper_kernel_pair(p->segregation, c->bin_k, c->bin_c32, kflags) != nullptr;
         c->bin_ilp = bin_schedule_rule(pair_ok, pair_mode, sched, max_chunk, c->cus, k64u16, tf0, occ_def, occ_ilp,
                                        c->stepper_block);
         // bin store: LDS-resident events, bounded by issue and LDS latency: every resident block helps
@@ -660,8 +661,7 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
     // off. Rotation replaces it.
     for (auto& ch : c->chunks) {
         // (paired lanes: owners only)
-        const uint32_t per_block =
-            c->bin_ilp == 3 ? c->stepper_block / 2 : (c->bin_ilp == 4 ? c->stepper_block / 4 : c->stepper_block);
+        const uint32_t per_block = c->bin_ilp == 3 ? c->stepper_block / 2 : c->stepper_block;
         const uint32_t need = (ch.n + per_block - 1) / per_block;
         ch.blocks = std::max<uint32_t>(1, std::min<uint32_t>(need, c->stepper_blocks_cap));
         const uint64_t lanes = (uint64_t)ch.blocks * c->stepper_block;
@@ -850,7 +850,7 @@ int ecdna_ssa_ctx_instance(const ecdna_ssa_ctx* c, ecdna_ssa_instance_t* out) {
     } else if (c->bin_k) {
         r.kernel = ECDNA_KERNEL_BINS;
         r.schedule = c->bin_ilp;
-        r.paired = c->bin_ilp == 3 ? 1 : (c->bin_ilp == 4 ? 2 : 0);
+        r.paired = c->bin_ilp == 3 ? 1 : 0;
         r.bin_kmax = c->bin_k;
         r.bin_c32 = (uint32_t)c->bin_c32;
         r.runtime_flags = (kernel_flags(p) & ecdna::kRuntimeFlagMask) ? 1 : 0;

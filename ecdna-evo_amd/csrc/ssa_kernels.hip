@@ -257,6 +257,9 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
             ch = target < cA ? 0u : (target < cB ? 1u : (target < cC ? 2u : 3u));
         else
             ch = target < cA ? 0u : 1u;
+#ifdef ECDNA_INJECT_EMPTY_NPLUS  // (fault-injection builds only, tools/inject_check.py: an N+ event with no N+ cell)
+        if (np == 0u) ch = BD ? 3u : 1u;
+#endif
 
         WordStream ws;
         ws.w2 = w.z;
@@ -286,6 +289,15 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
                 }
             }
             idx = (uint32_t)(m >> 32);
+            // the indexing invariant (ECDNA_REP_ERR_INTERNAL, ABI v11): an N+ event needs an N+ cell, and the pick
+            // stays below n+ (np == 0 gives idx 0 here). Unreachable under draw mapping v7; a broken channel would
+            // otherwise wrap np and index off the row (the r05e illegal address). The oracle returns the same code.
+            if (idx >= np) {
+                err = ECDNA_REP_ERR_INTERNAL;
+                stop = ECDNA_STOP_ERROR;
+                active = false;
+                continue;
+            }
             if (ch == 1u) {
                 if (idx == np - 1)
                     k = tail;
@@ -444,33 +456,11 @@ constexpr int kCpolSc1 = 16;  // buffer cache policy: sc1 (gfx940+ bit 4)
 #ifndef ECDNA_FF_STAY8
 #define ECDNA_FF_STAY8 7   // keep going while >= this many eighths of the entered lanes do
 #endif
-#ifndef ECDNA_FF_STAY8_QUAD
-#define ECDNA_FF_STAY8_QUAD 4  // quads (four events per step): keep going while >= this many eighths of the owners do
-#endif
-#ifndef ECDNA_FF_MAX_QUAD
-#define ECDNA_FF_MAX_QUAD 64  // quads: N- events per owner and fast-forward run at most
-#endif
 // the entry test is a mask of the wave-uniform iteration counter (ff_tick & (N - 1)): N must be a power of two
 static_assert(ECDNA_FF_TEST_EVERY > 0 && (ECDNA_FF_TEST_EVERY & (ECDNA_FF_TEST_EVERY - 1)) == 0,
               "ECDNA_FF_TEST_EVERY must be a power of two");
 constexpr uint32_t kFfMax = ECDNA_FF_MAX;  // N- fast-forward: events per full iteration at most
-constexpr uint32_t kFfMaxQuad = ECDNA_FF_MAX_QUAD;
 
-// DPP quad_perm broadcast of lane 4j + Q's value to lanes 4j .. 4j + 3 (one v_mov_b32_dpp)
-template <int Q>
-__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, Q * 0x55, 0xF, 0xF, false);
-}
-template <int Q>
-__device__ __forceinline__ float quad_bcast_f(float v) {
-    return __uint_as_float(quad_bcast<Q>(__float_as_uint(v)));
-}
-template <int Q>
-__device__ __forceinline__ double quad_bcast_d(double v) {
-    const uint64_t b = (uint64_t)__double_as_longlong(v);
-    return __longlong_as_double((long long)(((uint64_t)quad_bcast<Q>((uint32_t)(b >> 32)) << 32) |
-                                            quad_bcast<Q>((uint32_t)b)));
-}
 #ifdef ECDNA_ILP_BUILD
 #define ECDNA_DEV_STATIC static
 #else
@@ -643,11 +633,11 @@ __device__ __forceinline__ uint32_t vec_get(const uint4& v, int j) {
 
 // SCH: the build's schedule (no code): 0 occupancy-first, 1 max-ILP (ECDNA_ILP_BUILD), 2 occupancy-first
 // capped at 128 VGPRs so that four 256-lane workgroups fit a CU (K = 64 / u16 only, many replicates per lane)
-// PAIR (lone waves, DESIGN.md §5 "Paired lanes"): 1 = pairs: lane l < 32 of every wave owns a replicate, lane l + 32 is
-// its helper: in the N- fast-forward both compute a Philox block and soft log with the same instructions, the
-// owner's for event e and the helper's for e + 1, and the owner runs both events' state-dependent steps.
-// 2 = quads: lane 4j owns a replicate, lanes 4j + 1 .. 4j + 3 help: four events per fast-forward step ("Quads").
-template <bool BD, int SEG, int NG, bool C32, int BLK, int TF, int SCH, int PAIR = 0>
+// PAIR (lone waves, DESIGN.md §5 "Paired lanes"): lane l < 32 of every wave owns a replicate, lane l + 32 is its
+// helper: in the N- fast-forward both compute a Philox block and soft log with the same instructions, the owner's
+// for event e and the helper's for e + 1, and the owner runs both events' state-dependent steps. (Round 5's lane
+// quads, four lanes per replicate, were slower at every shard size and are gone, VERDICT r05 #7.)
+template <bool BD, int SEG, int NG, bool C32, int BLK, int TF, int SCH, bool PAIR = false>
 __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const StepperArgs a) {
     using L = BinLayout<NG, C32>;
     constexpr uint32_t K = L::kK;
@@ -660,12 +650,12 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
     const PhiloxKeys rk = philox_round_keys(k0, k1);  // event blocks: round keys in VGPRs
     // the Philox blocks' XOR3 as the compiler builtin (ssa_device.hpp xor3) in the K = 64 / 256 and paired instances
     // (C4, C5 shards: waves that drain or run alone); the issue-bound K = 32 kernel (C3) keeps the asm form
-    constexpr bool kB3 = NG >= 8 || PAIR != 0;
+    constexpr bool kB3 = NG >= 8 || PAIR;
     PhiloxEventPre pre{0u, 0u, 0u};  // the replicate-only part of round 0
     PATH_STATS_DECL;
     const uint32_t stop32 = a.stop_cells < 0xffffffffull ? (uint32_t)a.stop_cells : 0xffffffffu;
-    // PAIR: a helper serves lane - 32 (pairs) or lane 4j (quads) and never owns a replicate
-    const bool helper = PAIR == 2 ? (threadIdx.x & 3u) != 0u : (PAIR && (threadIdx.x & 63u) >= 32u);
+    // PAIR: a helper serves lane - 32 and never owns a replicate
+    const bool helper = PAIR && (threadIdx.x & 63u) >= 32u;
     // the large-k row capacity, held in a VGPR for the event path's one compare (left to the compiler, the event
     // loop's SGPR pressure had it reloaded from the kernel arguments in every iteration, with an lgkmcnt(0) wait
     // that also drained the wave's outstanding LDS reads)
@@ -1099,7 +1089,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
             const uint32_t n_in = (uint32_t)__builtin_popcountll(__ballot(active));
             ff_mode = n_in != 0u && (uint32_t)__builtin_popcountll(__ballot(heavy)) * 8u >= n_in * ECDNA_FF_ENTER8;
             CYC_ADD(4, ff_mode ? 1u : 0u);
-            if (PAIR == 1 && ff_mode) {
+            if (PAIR && ff_mode) {
                 // Paired steps (DESIGN.md §5 "Paired lanes"): every lane forms one Philox block and soft log with
                 // the same instructions, the owner (lane l) for its event e, the helper (lane l + 32) for the
                 // owner's e + 1 from the owner's replicate-only round-0 words; the owner pulls the helper's words
@@ -1212,116 +1202,6 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     }
                     go = cB;
                 }
-            } else if (PAIR == 2 && ff_mode) {
-                // Quads (DESIGN.md §5 "Quads"): lanes 4j .. 4j + 3 serve the replicate of owner lane 4j. Per step every
-                // lane forms one Philox block and soft log with the same instructions, lane 4j + q for the owner's event
-                // e + q (its own counter, advanced by 4 per step); the four channel words reach every lane of the quad
-                // (DPP quad_perm), and all four lanes evaluate the owner's state chain for events e .. e + 3 with the
-                // same values (n- -> f32 propensities -> f64 sums -> channel -> n-: the lanes of a wave run the same
-                // instructions anyway, so the chain costs the quad nothing extra); lane 4j + q divides its own soft log
-                // by its event's a0 (one division for four events), the quotients come back to every lane, and the time
-                // chain runs with each event's time test. The step commits the events up to the first that is not an N-
-                // event or fails a stop test, by selects: every lane of the quad holds the owner's state (broadcast at
-                // entry) and commits identically, so the quad stays in step. Same draws, same arithmetic, same order as
-                // the unpaired loop below: results are identical. A step is one basic block; the next step's blocks and
-                // soft-log table loads are issued ahead.
-                const uint32_t qlane = threadIdx.x & 3u;
-                const uint32_t quad0 = (threadIdx.x & 63u) & ~3u;  // the quad's owner lane within the wave
-                // the owner's replicate and state to its helpers (the helpers own nothing; their copies are scratch)
-                bool go = quad_bcast<0>(active ? 1u : 0u) != 0u;
-                pre = PhiloxEventPre{quad_bcast<0>(pre.x0), quad_bcast<0>(pre.x1), quad_bcast<0>(pre.x2)};
-                nm = quad_bcast<0>(nm);
-                e = quad_bcast<0>(e);
-                t = quad_bcast_d<0>(t);
-                t32 = quad_bcast_f<0>(t32);
-                if (hash_on) h = ((uint64_t)quad_bcast<0>((uint32_t)(h >> 32)) << 32) | quad_bcast<0>((uint32_t)h);
-                const float qb0 = quad_bcast_f<0>(rb0), qd0 = quad_bcast_f<0>(rd0);
-                const double qpb = quad_bcast_d<0>(pbf), qpd = quad_bcast_d<0>(pdf);
-                const uint32_t qnpf = quad_bcast<0>(npf);
-                uint32_t ctr = e + qlane;
-                uint4 wb = philox_event<kB3>(ctr, pre, rk);
-                SoftlogParts lp = softlog_begin(wb.x, logtab);
-#pragma unroll 1
-                for (uint32_t q = 0; q < kFfMaxQuad; q += 4) {
-                    // (owners only: the helpers carry their owner's go)
-                    if ((uint32_t)__builtin_popcountll(__ballot(go && qlane == 0u)) * 8u < n_in * ECDNA_FF_STAY8_QUAD)
-                        break;  // (uniform)
-                    CYC_ADD(5, 1);
-                    const float lg = softlog_end(lp);  // this lane's event e + qlane
-                    const uint4 wa = wb;
-                    ctr += 4u;  // the next step's words (events e + 4 + qlane), off this step's chain
-                    wb = philox_event<kB3>(ctr, pre, rk);
-                    lp = softlog_begin(wb.x, logtab);
-                    const uint32_t y0 = quad_bcast<0>(wa.y), y1 = quad_bcast<1>(wa.y), y2 = quad_bcast<2>(wa.y),
-                                   y3 = quad_bcast<3>(wa.y);
-                    // the state chain of events e .. e + 3 (time tests below): propensities, channel, n-
-                    const float f0 = (float)nm;
-                    const double c00 = (double)(qb0 * f0), c10 = c00 + qpb, c20 = c10 + (double)(qd0 * f0), A0 = c20 + qpd;
-                    const double x0 = chan_target(y0, A0);
-                    const bool g00 = x0 >= c00, g10 = x0 >= c10, g20 = x0 >= c20, dm0 = g10 & !g20;
-                    const float a00 = (float)A0;
-                    const bool ok0 = go & (e < a.max_iter) & (nm + qnpf < stop32) & (a00 > 0.0f) & (!g00 | dm0);
-                    const uint32_t nm1 = nm + (g00 ? 0u : 1u) - (dm0 ? 1u : 0u);
-                    const float f1 = (float)nm1;
-                    const double c01 = (double)(qb0 * f1), c11 = c01 + qpb, c21 = c11 + (double)(qd0 * f1), A1 = c21 + qpd;
-                    const double x1 = chan_target(y1, A1);
-                    const bool g01 = x1 >= c01, g11 = x1 >= c11, g21 = x1 >= c21, dm1 = g11 & !g21;
-                    const float a01 = (float)A1;
-                    const bool ok1 = (e + 1u < a.max_iter) & (nm1 + qnpf < stop32) & (a01 > 0.0f) & (!g01 | dm1);
-                    const uint32_t nm2 = nm1 + (g01 ? 0u : 1u) - (dm1 ? 1u : 0u);
-                    const float f2 = (float)nm2;
-                    const double c02 = (double)(qb0 * f2), c12 = c02 + qpb, c22 = c12 + (double)(qd0 * f2), A2 = c22 + qpd;
-                    const double x2 = chan_target(y2, A2);
-                    const bool g02 = x2 >= c02, g12 = x2 >= c12, g22 = x2 >= c22, dm2 = g12 & !g22;
-                    const float a02 = (float)A2;
-                    const bool ok2 = (e + 2u < a.max_iter) & (nm2 + qnpf < stop32) & (a02 > 0.0f) & (!g02 | dm2);
-                    const uint32_t nm3 = nm2 + (g02 ? 0u : 1u) - (dm2 ? 1u : 0u);
-                    const float f3 = (float)nm3;
-                    const double c03 = (double)(qb0 * f3), c13 = c03 + qpb, c23 = c13 + (double)(qd0 * f3), A3 = c23 + qpd;
-                    const double x3 = chan_target(y3, A3);
-                    const bool g03 = x3 >= c03, g13 = x3 >= c13, g23 = x3 >= c23, dm3 = g13 & !g23;
-                    const float a03 = (float)A3;
-                    const bool ok3 = (e + 3u < a.max_iter) & (nm3 + qnpf < stop32) & (a03 > 0.0f) & (!g03 | dm3);
-                    const uint32_t nm4 = nm3 + (g03 ? 0u : 1u) - (dm3 ? 1u : 0u);
-                    // this lane's event's quotient, then all four to every lane
-                    const float a0own = qlane == 0u ? a00 : (qlane == 1u ? a01 : (qlane == 2u ? a02 : a03));
-                    const float tau = div_in_range(lg, a0own);
-                    const float tau0 = quad_bcast_f<0>(tau), tau1 = quad_bcast_f<1>(tau), tau2 = quad_bcast_f<2>(tau),
-                                tau3 = quad_bcast_f<3>(tau);
-                    // the time chain: event e + q is tested against the time after e .. e + q - 1
-                    const double t1 = t + (double)tau0, t2 = t1 + (double)tau1, t3 = t2 + (double)tau2,
-                                 t4 = t3 + (double)tau3;
-                    const float s1 = t32 + tau0, s2 = s1 + tau1, s3 = s2 + tau2, s4 = s3 + tau3;
-                    const bool ov0 = f32t ? (t32 >= a.max_time32) : (t >= a.max_time);
-                    const bool ov1 = f32t ? (s1 >= a.max_time32) : (t1 >= a.max_time);
-                    const bool ov2 = f32t ? (s2 >= a.max_time32) : (t2 >= a.max_time);
-                    const bool ov3 = f32t ? (s3 >= a.max_time32) : (t3 >= a.max_time);
-                    const bool k1 = ok0 & !ov0, k2 = k1 & ok1 & !ov1, k3 = k2 & ok2 & !ov2, k4 = k3 & ok3 & !ov3;
-                    // commit (an N- event pushes its w2, w3 onto the spare stack: after the last committed event e + k - 1
-                    // the stack holds exactly that event's two words, lane 4j + k - 1's)
-                    const uint32_t kk = (k1 ? 1u : 0u) + (k2 ? 1u : 0u) + (k3 ? 1u : 0u) + (k4 ? 1u : 0u);
-                    const int src = (int)((quad0 + (kk ? kk - 1u : 0u)) << 2);
-                    const uint32_t sz = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)wa.z);
-                    const uint32_t sw = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)wa.w);
-                    sp0 = k1 ? sw : sp0;
-                    sp1 = k1 ? sz : sp1;
-                    nsp = k1 ? 2u : nsp;
-                    nm = k4 ? nm4 : (k3 ? nm3 : (k2 ? nm2 : (k1 ? nm1 : nm)));
-                    n_dm += ((k1 & dm0) ? 1u : 0u) + ((k2 & dm1) ? 1u : 0u) + ((k3 & dm2) ? 1u : 0u) + ((k4 & dm3) ? 1u : 0u);
-                    e += kk;
-                    if (f32t)
-                        t32 = k4 ? s4 : (k3 ? s3 : (k2 ? s2 : (k1 ? s1 : t32)));
-                    else
-                        t = k4 ? t4 : (k3 ? t3 : (k2 ? t2 : (k1 ? t1 : t)));
-                    if (hash_on) {
-                        const uint64_t hA = (h ^ ((uint64_t)g00 + (uint64_t)g10 + (uint64_t)g20)) * kFnvPrime;
-                        const uint64_t hB = (hA ^ ((uint64_t)g01 + (uint64_t)g11 + (uint64_t)g21)) * kFnvPrime;
-                        const uint64_t hC = (hB ^ ((uint64_t)g02 + (uint64_t)g12 + (uint64_t)g22)) * kFnvPrime;
-                        const uint64_t hD = (hC ^ ((uint64_t)g03 + (uint64_t)g13 + (uint64_t)g23)) * kFnvPrime;
-                        h = k4 ? hD : (k3 ? hC : (k2 ? hB : (k1 ? hA : h)));
-                    }
-                    go = k4;
-                }
             } else if (ff_mode) {
                 bool go = active;
 #pragma unroll 1
@@ -1417,7 +1297,12 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
             // the channel as the three compares' lane masks (no integer channel on the event path; it is formed
             // only for the event hash): ProliferateNMinus !gA, ProliferateNPlus gA & !gB, DeathNMinus gB & !gC,
             // DeathNPlus gC
-            const bool gA = target >= cA, gB = BD && target >= cB, gC = BD && target >= cC;
+#ifdef ECDNA_INJECT_EMPTY_NPLUS  // (fault-injection builds only, tools/inject_check.py: an N+ event with no N+ cell)
+            const bool inj = TF != 0 && np == 0u;
+#else
+            constexpr bool inj = false;
+#endif
+            const bool gA = inj || target >= cA, gB = inj || (BD && target >= cB), gC = inj || (BD && target >= cC);
             const bool prolif = gA && !gB;
             const bool death_nm = gB && !gC;
             const bool nplus_ev = prolif || gC;  // ProliferateNPlus or DeathNPlus: a cell is picked
@@ -1544,6 +1429,11 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
             CYC_MARK(11);
             // checked_mul panic (src/proliferation.rs:63-67)
             ev_err = (k > 32767u) ? (uint32_t)ECDNA_REP_ERR_OVERFLOW : ev_err;
+            // the indexing invariant (ECDNA_REP_ERR_INTERNAL, ABI v11), in the runtime-flags instances (TF = 1; the
+            // bench's TF = 0 instances keep their event path): an N+ event needs an N+ cell and a pick below n+
+            // (np == 0 gives idx 0). Unreachable under draw mapping v7; a broken channel would otherwise swap_remove
+            // from an empty large-k row and wrap nb. Any event, death included; the oracle returns the same code.
+            const bool internal = TF != 0 && nplus_ev && idx >= np;
             // daughters (none for a death): [k1, k2] on an even split, [n] on an uneven one
             const uint32_t da = (un == 0u) ? k1v : n;
             const uint32_t db = n - k1v;
@@ -1562,8 +1452,8 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     ev_err = ECDNA_REP_ERR_CELL_CAP;
             }
             CYC_MARK(12);
-            if (prolif && ev_err) {  // the event is not applied; the replicate stops (rare)
-                err = ev_err;
+            if ((prolif && ev_err) || internal) {  // the event is not applied; the replicate stops (rare)
+                err = internal ? (uint32_t)ECDNA_REP_ERR_INTERNAL : ev_err;
                 stop = ECDNA_STOP_ERROR;
                 active = false;
             } else {
@@ -1870,7 +1760,9 @@ __global__ void __launch_bounds__(kHistBlock) ssa_hist_bags(const HistArgs a) {
                     uint32_t c[16];
 #pragma unroll
                     for (uint32_t i = 0; i < 16u; ++i) c[i] = i0 + i < nq ? counter(base + i0 + i, lane + 64u * m) : 0u;
-                    uint32_t sum = 0;
+                    // (u64: a u32 counter holds up to cell_cap < 2^32 cells of one bin, so 16 replicates' sum can
+                    // pass 2^32)
+                    uint64_t sum = 0;
 #pragma unroll
                     for (uint32_t i = 0; i < 16u; ++i) sum += c[i];
                     acc[m] += sum;
@@ -1998,22 +1890,18 @@ const void* bin_stepper_kernel_ilp(int birth_death, int segregation, uint32_t bi
 
 // paired lanes (PAIR = true; birth-death only, its N- fast-forward is what pairs): [TF][segregation][K = 32 / u32,
 // K = 64 / u16, K = 64 / u32]
-#define ECDNA_BIN_PAIR_SEG(SEG, TF, G)                                                                       \
-    {(const void*)ssa_stepper_bins<true, SEG, 4, true, kStepperBlock, TF, ECDNA_SCH, G>,                    \
-     (const void*)ssa_stepper_bins<true, SEG, 8, false, kStepperBlock, TF, ECDNA_SCH, G>,                   \
-     (const void*)ssa_stepper_bins<true, SEG, 8, true, kStepperBlock, TF, ECDNA_SCH, G>}
-#define ECDNA_BIN_PAIR_TF(TF, G) \
-    {ECDNA_BIN_PAIR_SEG(0, TF, G), ECDNA_BIN_PAIR_SEG(1, TF, G), ECDNA_BIN_PAIR_SEG(2, TF, G), ECDNA_BIN_PAIR_SEG(3, TF, G)}
-// [pairs | quads][TF][segregation][K = 32 / u32, K = 64 / u16, K = 64 / u32]
-static const void* const kBinPairTable[2][2][4][3] = {{ECDNA_BIN_PAIR_TF(0, 1), ECDNA_BIN_PAIR_TF(1, 1)},
-                                                      {ECDNA_BIN_PAIR_TF(0, 2), ECDNA_BIN_PAIR_TF(1, 2)}};
+#define ECDNA_BIN_PAIR_SEG(SEG, TF)                                                                          \
+    {(const void*)ssa_stepper_bins<true, SEG, 4, true, kStepperBlock, TF, ECDNA_SCH, true>,                 \
+     (const void*)ssa_stepper_bins<true, SEG, 8, false, kStepperBlock, TF, ECDNA_SCH, true>,                \
+     (const void*)ssa_stepper_bins<true, SEG, 8, true, kStepperBlock, TF, ECDNA_SCH, true>}
+#define ECDNA_BIN_PAIR_TF(TF) \
+    {ECDNA_BIN_PAIR_SEG(0, TF), ECDNA_BIN_PAIR_SEG(1, TF), ECDNA_BIN_PAIR_SEG(2, TF), ECDNA_BIN_PAIR_SEG(3, TF)}
+static const void* const kBinPairTable[2][4][3] = {ECDNA_BIN_PAIR_TF(0), ECDNA_BIN_PAIR_TF(1)};
 
-// group = 2: pairs, 4: quads
-const void* bin_stepper_kernel_pair(int segregation, uint32_t bin_k, int c32, uint32_t flags, int group) {
+const void* bin_stepper_kernel_pair(int segregation, uint32_t bin_k, int c32, uint32_t flags) {
     const int tf = (flags & kRuntimeFlagMask) ? 1 : 0;
-    const int g = group == 4 ? 1 : 0;
-    if (bin_k == 32 && c32) return kBinPairTable[g][tf][segregation & 3][0];
-    if (bin_k == 64) return kBinPairTable[g][tf][segregation & 3][c32 ? 2 : 1];
+    if (bin_k == 32 && c32) return kBinPairTable[tf][segregation & 3][0];
+    if (bin_k == 64) return kBinPairTable[tf][segregation & 3][c32 ? 2 : 1];
     return nullptr;
 }
 #else
@@ -2022,8 +1910,7 @@ const void* stepper_kernel(int birth_death, int segregation, int window) {
 }
 
 const void* bin_stepper_kernel(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags, int ilp) {
-    if (ilp == 3 || ilp == 4)
-        return birth_death ? bin_stepper_kernel_pair(segregation, bin_k, c32, flags, ilp == 4 ? 4 : 2) : nullptr;
+    if (ilp == 3) return birth_death ? bin_stepper_kernel_pair(segregation, bin_k, c32, flags) : nullptr;
     if (ilp == 2 && bin_k == 64 && !c32) {
         const int tf = (flags & kRuntimeFlagMask) ? 1 : 0;
         return kBinOcc4Table[tf][birth_death ? 1 : 0][segregation & 3];

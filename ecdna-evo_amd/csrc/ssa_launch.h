@@ -131,9 +131,8 @@ const void* bin_stepper_kernel(int birth_death, int segregation, uint32_t bin_k,
 const void* bin_stepper_kernel_ilp(int birth_death, int segregation, uint32_t bin_k, int c32, uint32_t flags);
 // ilp = 3: the max-ILP schedule with paired lanes (lane l < 32 owns a replicate, lane l + 32 helps its N-
 // fast-forward; birth-death, K = 32 / u32 or K = 64): nullptr where no such instance exists. A paired
-// workgroup of kStepperBlock lanes runs kStepperBlock / 2 replicates at a time. ilp = 4: quads (lane 4j owns a
-// replicate, lanes 4j + 1 .. 4j + 3 help): kStepperBlock / 4 replicates per workgroup. group: 2 or 4.
-const void* bin_stepper_kernel_pair(int segregation, uint32_t bin_k, int c32, uint32_t flags, int group);
+// workgroup of kStepperBlock lanes runs kStepperBlock / 2 replicates at a time.
+const void* bin_stepper_kernel_pair(int segregation, uint32_t bin_k, int c32, uint32_t flags);
 int bin_stepper_block(uint32_t bin_k);
 hipError_t launch_bin_stepper(const StepperArgs& a, int birth_death, int segregation, uint32_t bin_k, int c32, int ilp,
                               uint32_t blocks, hipStream_t stream);

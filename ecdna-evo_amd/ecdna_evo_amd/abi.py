@@ -14,7 +14,10 @@ from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
-ABI_VERSION = 10
+ABI_VERSION = 11
+# the oldest library an A/B may load under ECDNA_SSA_ABI_ANY=1: the same Params layout as this ABI (v10 appended
+# max_workgroups; v11 changed no struct)
+ABI_SAME_LAYOUT_SINCE = 10
 
 # ecdna_process_t (ProcessType, src/clap_app.rs:311-315)
 PURE_BIRTH = 0
@@ -40,7 +43,7 @@ STOP_NONE, STOP_MAX_CELLS, STOP_MAX_TIME, STOP_MAX_ITER, STOP_ABSORBING, STOP_ER
 STOP_NAMES = ["None", "MaxCells", "MaxTime", "MaxIter", "Absorbing", "Error"]
 
 # ecdna_rep_error_t
-REP_OK, REP_ERR_OVERFLOW, REP_ERR_EMPTY, REP_ERR_CELL_CAP, REP_ERR_REJECTION = range(5)
+REP_OK, REP_ERR_OVERFLOW, REP_ERR_EMPTY, REP_ERR_CELL_CAP, REP_ERR_REJECTION, REP_ERR_INTERNAL = range(6)
 
 FLAG_TIME_F32 = 0x1
 FLAG_BD_CAP_COMPAT = 0x2
@@ -101,12 +104,12 @@ FLAG_BIN_STORE = 0x20  # cells binned by copy number; bin_kmax
 # the reference's own draw structure (ChaCha8 streams seed*10+r, first reaction, rand_distr samplers, f32 time;
 # row store only): seed for seed the oracle's compat mode
 FLAG_REFERENCE_DRAWS = 0x40
+FLAG_ALL = 0x7F  # every defined flag (ecdna_ssa_ctx_create rejects other bits since ABI v11)
 
 
 # ecdna_ssa_instance_t (ABI v7): the kernel instance a context launches (ecdna_ssa_ctx_instance)
 KERNEL_KINDS = {0: "ssa_stepper (rows)", 1: "ssa_stepper_bins (bins)", 2: "ssa_stepper_refdraws (reference draws)"}
-SCHEDULE_NAMES = {-1: "n/a", 0: "occupancy-first", 1: "max-ILP", 2: "occupancy-first, 128-VGPR cap", 3: "max-ILP, paired lanes",
-                  4: "max-ILP, lane quads"}
+SCHEDULE_NAMES = {-1: "n/a", 0: "occupancy-first", 1: "max-ILP", 2: "occupancy-first, 128-VGPR cap", 3: "max-ILP, paired lanes"}
 
 
 class Instance(C.Structure):

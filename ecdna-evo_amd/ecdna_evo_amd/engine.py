@@ -122,9 +122,11 @@ def lib():
     L.ecdna_ssa_ctx_reduce.argtypes = [C.c_void_p, C.c_void_p]
     L.ecdna_ssa_ctx_reduce.restype = C.c_int
     ver = L.ecdna_ssa_abi_version()
-    # (a same-box A/B, tools/ab_build.sh, may load a library of an earlier ABI version whose layout is unchanged:
-    # ECDNA_SSA_ABI_ANY=1 accepts it from 8 on; results then follow that library's draw mapping)
-    if ver != abi.ABI_VERSION and not (os.environ.get("ECDNA_SSA_ABI_ANY") == "1" and ver >= 8):
+    # (a same-box A/B, tools/ab_build.sh, may load a library of an earlier ABI version whose Params layout is this
+    # one's: ECDNA_SSA_ABI_ANY=1 accepts versions ABI_SAME_LAYOUT_SINCE .. ABI_VERSION, never a newer one;
+    # results then follow that library's draw mapping)
+    any_ok = os.environ.get("ECDNA_SSA_ABI_ANY") == "1" and abi.ABI_SAME_LAYOUT_SINCE <= ver <= abi.ABI_VERSION
+    if ver != abi.ABI_VERSION and not any_ok:
         raise EngineError("ABI version mismatch between libecdna_ssa.so and ecdna_evo_amd.abi")
     _lib = L
     return L

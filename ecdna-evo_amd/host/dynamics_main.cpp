@@ -41,6 +41,7 @@ struct Options {
     std::string segregation_name = "binomial";
     std::string growth = "exponential";
     float b0 = 1.f, b1 = 1.f;
+    std::string b0_arg = "1", b1_arg = "1", d0_arg = "0", d1_arg = "0";  // as given (for error messages)
     bool has_d0 = false, has_d1 = false;
     float d0 = 0.f, d1 = 0.f;
     bool has_years = false, has_cells = false;
@@ -168,14 +169,18 @@ Options parse(int argc, char** argv) {
             if (o.growth != "exponential" && o.growth != "constant")
                 usage_error("invalid value '" + o.growth + "' for '--growth <GROWTH>'");
         } else if (a == "--b0") {
-            o.b0 = parse_f32(a, need(a));
+            o.b0_arg = need(a);
+            o.b0 = parse_f32(a, o.b0_arg);
         } else if (a == "--b1") {
-            o.b1 = parse_f32(a, need(a));
+            o.b1_arg = need(a);
+            o.b1 = parse_f32(a, o.b1_arg);
         } else if (a == "--d0") {
-            o.d0 = parse_f32(a, need(a));
+            o.d0_arg = need(a);
+            o.d0 = parse_f32(a, o.d0_arg);
             o.has_d0 = true;
         } else if (a == "--d1") {
-            o.d1 = parse_f32(a, need(a));
+            o.d1_arg = need(a);
+            o.d1 = parse_f32(a, o.d1_arg);
             o.has_d1 = true;
         } else if (a == "-y" || a == "--years") {
             o.years = parse_u64(a, need(a));
@@ -258,11 +263,17 @@ Options parse(int argc, char** argv) {
     if (o.reference_draws) o.rows = true;
     // The engine's rate range (include/ecdna_ssa.h, since ABI v8): 0 or [2^-60, 2^60]; a divergence from the
     // reference, which takes any f32. Reported here as a usage error, before any GPU work.
-    const std::pair<const char*, float> rate_args[] = {{"--b0 <RATE>", o.b0}, {"--b1 <RATE>", o.b1}, {"--d0 <RATE>", o.d0},
-                                                       {"--d1 <RATE>", o.d1}};
+    // (the message echoes the argument as given: std::to_string prints 6 fixed decimals, "1e-20" as "0.000000")
+    struct RateArg {
+        const char* flag;
+        float value;
+        const std::string* text;
+    };
+    const RateArg rate_args[] = {{"--b0 <RATE>", o.b0, &o.b0_arg}, {"--b1 <RATE>", o.b1, &o.b1_arg},
+                                 {"--d0 <RATE>", o.d0, &o.d0_arg}, {"--d1 <RATE>", o.d1, &o.d1_arg}};
     for (const auto& ra : rate_args)
-        if (!(ra.second == 0.f || (ra.second >= 0x1p-60f && ra.second <= 0x1p60f)))
-            usage_error("invalid value '" + std::to_string(ra.second) + "' for '" + ra.first +
+        if (!(ra.value == 0.f || (ra.value >= 0x1p-60f && ra.value <= 0x1p60f)))
+            usage_error("invalid value '" + *ra.text + "' for '" + ra.flag +
                         "': rates must be 0 or in [2^-60, 2^60] (8.67e-19 .. 1.15e18) for this engine");
     return o;
 }

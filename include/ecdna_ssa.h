@@ -43,10 +43,12 @@
 extern "C" {
 #endif
 
-/* ABI v10: ecdna_ssa_params_t.max_workgroups (a cap on the persistent grid, for contexts that share a GPU
- * concurrently) appended; draw mapping v7 as in v9 (the channel from all 32 bits of the event's word over f64
- * cumulative propensities; results differ from v8 seed for seed). */
-#define ECDNA_SSA_ABI_VERSION 10
+/* ABI v11: ECDNA_REP_ERR_INTERNAL (a replicate whose event would pick from an empty N+ set stops instead of
+ * indexing off its row); unknown flag bits are rejected; the lane-quad schedule (instance schedule 4) is gone.
+ * The Params layout and draw mapping v7 are those of v10 (v10 appended ecdna_ssa_params_t.max_workgroups, a cap on
+ * the persistent grid for contexts that share a GPU; v9 took the channel from all 32 bits of the event's word over
+ * f64 cumulative propensities). */
+#define ECDNA_SSA_ABI_VERSION 11
 
 /* Process type — ProcessType (src/clap_app.rs:311-315); chosen as BirthDeath
  * when d0 > 0 or d1 > 0 (src/clap_app.rs:163-174, 194-200). */
@@ -91,7 +93,12 @@ typedef enum {
     ECDNA_REP_ERR_EMPTY = 2,      /* empty initial distribution: ensure!, src/process.rs:88, 232 */
     ECDNA_REP_ERR_CELL_CAP = 3,   /* N+ row would exceed cell_cap (the reference grows a Vec), or the
                                      bin store's large-k row would exceed big_cap */
-    ECDNA_REP_ERR_REJECTION = 4   /* BinomialNoUneven loop exceeded 4096 redraws (p < 2^-4096) */
+    ECDNA_REP_ERR_REJECTION = 4,  /* BinomialNoUneven loop exceeded 4096 redraws (p < 2^-4096) */
+    ECDNA_REP_ERR_INTERNAL = 5    /* an N+ event drawn with no N+ cell, or a cell index past n+ (ABI v11): the event
+                                     is not applied and the replicate stops. Unreachable under draw mapping v7 (a
+                                     zero-propensity channel is never drawn); the guard keeps a broken invariant
+                                     from indexing off the row. The reference's pick_remove_random_nplus returns an
+                                     error on an empty N+ set (src/proliferation.rs:57). */
 } ecdna_rep_error_t;
 
 /* Flags (ecdna_ssa_params_t.flags). */
@@ -119,6 +126,8 @@ typedef enum {
  * calls agree with them wherever glibc rounds correctly). A correctness path for seed-for-seed comparison
  * with the reference semantics, not a fast path. */
 #define ECDNA_FLAG_REFERENCE_DRAWS 0x40u
+/* Every defined flag; ecdna_ssa_ctx_create rejects other bits (ABI v11). */
+#define ECDNA_FLAG_ALL 0x7fu
 
 /* API return codes. */
 #define ECDNA_OK 0
@@ -314,10 +323,8 @@ typedef enum {
 typedef struct {
     int32_t kernel;            /* ecdna_kernel_kind_t */
     int32_t schedule;          /* bin stepper: 0 occupancy-first, 1 max-ILP, 2 occupancy-first capped at 128
-                                  VGPRs (K = 64 / u16), 3 max-ILP with paired lanes, 4 max-ILP with quads; -1 for
-                                  the other kernels */
-    int32_t paired;            /* 1: lane l < 32 owns a replicate, lane l + 32 helps its N- fast-forward (pairs);
-                                  2: lane 4j owns one, lanes 4j + 1 .. 4j + 3 help (quads) */
+                                  VGPRs (K = 64 / u16), 3 max-ILP with paired lanes; -1 for the other kernels */
+    int32_t paired;            /* 1: lane l < 32 owns a replicate, lane l + 32 helps its N- fast-forward (pairs) */
     int32_t rotation;          /* number of chunks whose replicates rotate through the lanes */
     int32_t rot_tick_log2;     /* rotation tick (loop iterations, log2) */
     int32_t drain_control;     /* number of chunks whose youngest wave slots stop admitting replicates early */

@@ -590,6 +590,14 @@ static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16
         event_block(p->seed, rid, e, w);
         /* direct method: channel by w1 against the cumulative propensities */
         const int ch = channel_of(c, chan_target(w[1], A));
+        /* an N+ event with no N+ cell: the engine's guard (ECDNA_REP_ERR_INTERNAL, ABI v11). Unreachable under draw
+         * mapping v7 (a zero-propensity channel is never drawn); the reference's pick_remove_random_nplus errors on an
+         * empty N+ set (src/proliferation.rs:55-57). The event is not applied. */
+        if ((ch & 1) && nplus == 0) {
+            err = ECDNA_REP_ERR_INTERNAL;
+            stop = ECDNA_STOP_ERROR;
+            continue;
+        }
         float tau = oracle_softlog_neg(w[0]) / a0; /* the correctly rounded f32 quotient */
         wstream ws;
         ws_init(&ws, p->seed, rid, e, w[2], w[3]);
@@ -835,7 +843,7 @@ int oracle_run_compat(const ecdna_ssa_params_t* p, ecdna_rep_summary_t* out_summ
 
 int oracle_increase_nplus(oracle_distr_t* d, int seg, uint64_t seed, uint64_t rid, uint32_t e, uint32_t* k1,
                           uint32_t* k2, int* is_uneven) {
-    if (d->len == 0) return -1; /* pick_remove_random_nplus fails on no N+ cells (src/proliferation.rs:55-57) */
+    if (d->len == 0) return ECDNA_REP_ERR_INTERNAL; /* pick_remove_random_nplus fails on no N+ cells (src/proliferation.rs:55-57) */
     uint32_t w[4];
     event_block(seed, rid, e, w);
     wstream ws;
@@ -845,7 +853,7 @@ int oracle_increase_nplus(oracle_distr_t* d, int seg, uint64_t seed, uint64_t ri
 }
 
 int oracle_decrease_nplus(oracle_distr_t* d, uint64_t seed, uint64_t rid, uint32_t e) {
-    if (d->len == 0) return -1;
+    if (d->len == 0) return ECDNA_REP_ERR_INTERNAL; /* as increase_nplus: the engine's guard's code */
     uint32_t w[4];
     event_block(seed, rid, e, w);
     wstream ws;

@@ -65,23 +65,57 @@ def test_workload_bin_kmax_defaults(workload, kmax):
     assert bench.workload_spec(0, 8, total, workload=workload, store="rows").bin_kmax == 0
 
 
-def test_c5_bin_kmax_by_replicates_per_gpu():
-    """C5 takes K = 32 where a GPU holds more replicates than K = 64's grid has lanes (the whole run on one GPU), and
-    K = 64 for the 8-, 4- and 2-GPU shards (profiles/r04s_c5_kmax.txt)."""
-    total = bench.WORKLOADS["c5"][0]
-    assert bench.workload_spec(0, total, total, workload="c5").bin_kmax == 32
-    for gpus in (2, 4, 8):
-        assert bench.workload_spec(0, total // gpus, total, workload="c5").bin_kmax == 64
-    assert bench.workload_spec(0, total, total, workload="c5", bin_kmax=64).bin_kmax == 64
+def _kmax_by_id(workload, world, **kw):
+    """{global replicate id: K it runs at} over every rank's contexts of a `world`-GPU bench run (bench.rank_parts)."""
+    ids, ks = [], []
+    for rank in range(world):
+        rp = bench.rank_parts(workload, world, rank, **kw)
+        assert sum(sp.n_replicates for sp, _ in rp.parts) == rp.spec.n_replicates
+        for sp, _ in rp.parts:
+            ids.append(sp.replicate_ids())
+            ks.append(np.full(sp.n_replicates, sp.bin_kmax, dtype=np.uint16))
+    ids, ks = np.concatenate(ids), np.concatenate(ks)
+    order = np.argsort(ids, kind="stable")
+    return ids[order], ks[order]
 
 
-@pytest.mark.parametrize("world", sorted(bench.C4_SPLIT_CAPS))
+@pytest.mark.parametrize("workload,kw", [("c5", {}), ("c4", {}), ("c2", {}), ("c3", {"scaling": "strong"}),
+                                         ("c4", {"k0_split": "off"}), ("c5", {"bin_kmax": 32})])
+def test_every_gpu_count_runs_each_replicate_at_the_same_k(workload, kw):
+    """K is part of the draw mapping, so a replicate's results depend on its id and
+    the workload only if every GPU count runs it at the same K. For each fixed-total workload, every rank of every GPU
+    count from 1 to 8 (and 16) together runs each id exactly once and at the K of the one-GPU run: C5 at K = 64 (round
+    5 took K = 32 on one GPU only), C4's k0 = 128 sets at K = 256 under the k0 split at every count (round 5 split only
+    at 1, 2, 4 and 8)."""
+    ids1, k1 = _kmax_by_id(workload, 1, **kw)
+    assert len(ids1) == bench.WORKLOADS[workload][0] if workload != "c3" else len(ids1) == 1 << 20
+    for world in (2, 3, 4, 5, 6, 7, 8, 16):
+        ids, k = _kmax_by_id(workload, world, **kw)
+        np.testing.assert_array_equal(ids, ids1, err_msg=f"{workload} at {world} GPUs: ids")
+        np.testing.assert_array_equal(k, k1, err_msg=f"{workload} at {world} GPUs: K per replicate")
+    if workload == "c5":
+        assert set(np.unique(k1)) == {kw.get("bin_kmax", 64)}
+    if workload == "c4" and not kw:
+        assert set(np.unique(k1)) == {64, bench.C4_SPLIT_KMAX} and np.count_nonzero(k1 == 256) == len(k1) // 8
+
+
+def test_c4_split_caps_cover_every_gpu_count():
+    """The k0 split's grid caps (speed only) for GPU counts without a measured entry: the nearest measured count
+    below."""
+    assert bench.c4_split_caps(3) == bench.C4_SPLIT_CAPS[2]
+    assert bench.c4_split_caps(7) == bench.C4_SPLIT_CAPS[4]
+    assert bench.c4_split_caps(16) == bench.C4_SPLIT_CAPS[8]
+    for g, caps in bench.C4_SPLIT_CAPS.items():
+        assert bench.c4_split_caps(g) == caps
+
+
+@pytest.mark.parametrize("world", sorted(set(bench.C4_SPLIT_CAPS) | {3, 5}))
 def test_c4_k0_split_parts_partition_each_shard(world):
     """shard.k0_split on bench's C4 shards: two parts that together hold the shard's replicates in
     local order, the second exactly those of the k0 = 128 sets (K = 256), the first the rest (K = 64), each with
-    its workgroup cap from bench.C4_SPLIT_CAPS."""
+    its workgroup cap from bench.c4_split_caps (at any GPU count)."""
     total = bench.WORKLOADS["c4"][0]
-    caps = bench.C4_SPLIT_CAPS[world]
+    caps = bench.c4_split_caps(world)
     for rank in sorted({0, world - 1}):
         first, n, stride = shard.interleaved_range(rank, world, total)
         spec = bench.workload_spec(first, n, total, workload="c4", stride=stride)

@@ -140,15 +140,15 @@ def test_c4_bench_whole_instance_bit_exact(engine_mod, oracle_mod):
 
 @pytest.mark.gpu
 def test_c5_bench_whole_instance_bit_exact(engine_mod, oracle_mod):
-    """C5 on one GPU as `bench.py --workload c5` runs it (262,144 replicates, K = 32 with u32 counters since r04s:
-    four workgroups per CU, one replicate per lane; large-k row 2^16): the max-ILP schedule, unpaired; replicates
-    0..3 and two from the end (about 2e7 events each, to 1e6 cells) equal the oracle."""
+    """C5 on one GPU as `bench.py --workload c5` runs it (262,144 replicates, K = 64 with u32 counters, the K of its
+    shards since round 6: two workgroups per CU, two replicates per lane; large-k row 2^16): the max-ILP schedule,
+    unpaired; replicates 0..3 and two from the end (about 2e7 events each, to 1e6 cells) equal the oracle."""
     bench = _bench()
     spec = bench.workload_spec(0, 262_144, 262_144, workload="c5")
-    assert spec.flags == abi.FLAG_BIN_STORE and spec.bin_kmax == 32 and spec.big_cap == 1 << 16
+    assert spec.flags == abi.FLAG_BIN_STORE and spec.bin_kmax == 64 and spec.big_cap == 1 << 16
     ins, res = _run_with_instance(engine_mod, spec)
-    assert (ins["kernel"], ins["schedule"], ins["paired"], ins["bin_kmax"], ins["bin_c32"]) == (1, 1, 0, 32, 1), ins
-    assert ins["blocks_per_cu"] == 4 and ins["runtime_flags"] == 0, ins
+    assert (ins["kernel"], ins["schedule"], ins["paired"], ins["bin_kmax"], ins["bin_c32"]) == (1, 1, 0, 64, 1), ins
+    assert ins["blocks_per_cu"] == 2 and ins["runtime_flags"] == 0, ins
     s = res.summaries
     assert np.all(s["error"] == 0) and np.all(s["stop_reason"] == abi.STOP_MAX_CELLS)
     _compare_sample(res, spec, oracle_mod, 0, 4, threads=4)
@@ -211,3 +211,64 @@ def test_instance_reports_the_launched_grid_of_an_underfilled_paired_run(engine_
     finally:
         del os.environ["ECDNA_SSA_MAX_BLOCKS"]
     assert ins3["grid_lanes"] == 16 * 256, ins3
+
+
+def _rank_summaries(engine_mod, workload, world, rank, **kw):
+    """(global ids, summaries) of every context bench.py's rank `rank` of `world` launches (bench.rank_parts), run one
+    after another on this GPU (results never depend on the grid, the stream or what else runs)."""
+    bench = _bench()
+    rp = bench.rank_parts(workload, world, rank, **kw)
+    ids, summ = [], []
+    for sp, _ in rp.parts:
+        res = engine_mod.run(sp)
+        assert np.all(res.summaries["error"] == 0)
+        ids.append(sp.replicate_ids())
+        summ.append(res.summaries)
+    return np.concatenate(ids), np.concatenate(summ)
+
+
+def _assert_same_replicates(ids_a, summ_a, ids_b, summ_b, what):
+    """every replicate of b is in a, with the same summary bit for bit (the f64 time as bits)"""
+    order = np.argsort(ids_a, kind="stable")
+    idx = order[np.minimum(np.searchsorted(ids_a[order], ids_b), len(ids_a) - 1)]
+    np.testing.assert_array_equal(ids_a[idx], ids_b, err_msg=f"{what}: ids")
+    for f in summ_b.dtype.names:
+        a, b = summ_a[f][idx], summ_b[f]
+        if f == "time":
+            a, b = a.view(np.uint64), b.view(np.uint64)
+        np.testing.assert_array_equal(a, b, err_msg=f"{what}: {f}")
+
+
+@pytest.mark.gpu
+def test_c5_8gpu_shard_equals_the_one_gpu_run(engine_mod):
+    """the C5 8-GPU rank-0 shard (32,768 replicates, paired lanes) and the same ids inside the one-GPU
+    bench spec (262,144 replicates, unpaired max-ILP) give the same summaries bit for bit: one K (64) for every GPU
+    count (round 5 ran the one-GPU C5 at K = 32, a different draw mapping). The real shard and whole-run replicate
+    counts, so the real instances; the cell cap 1e5 instead of 1e6 (u32 counters as at 1e6) keeps the test short."""
+    ids1, s1 = _rank_summaries(engine_mod, "c5", 1, 0, max_cells=100_000)
+    ids8, s8 = _rank_summaries(engine_mod, "c5", 8, 0, max_cells=100_000)
+    assert len(ids1) == 262_144 and len(ids8) == 32_768
+    _assert_same_replicates(ids1, s1, ids8, s8, "C5 8-GPU rank 0 vs 1 GPU")
+    assert np.all(s8["stop_reason"] == abi.STOP_MAX_CELLS)
+
+
+@pytest.mark.gpu
+def test_c4_3gpu_shard_equals_the_one_gpu_run(engine_mod):
+    """a C4 shard at a GPU count without measured split caps (3: rank 1's 1,398,101 interleaved
+    replicates, split by k0 with the caps of 2 GPUs) against the one-GPU bench run of all 4,194,304 (split with the
+    caps of 1 GPU): the same summaries bit for bit, the k0 = 128 replicates at K = 256 on both sides (round 5 split
+    only at 1, 2, 4 and 8 GPUs, so a 3-GPU shard ran them at K = 64)."""
+    ids1, s1 = _rank_summaries(engine_mod, "c4", 1, 0)
+    ids3, s3 = _rank_summaries(engine_mod, "c4", 3, 1)
+    assert len(ids1) == 4_194_304 and len(ids3) == 1_398_101
+    _assert_same_replicates(ids1, s1, ids3, s3, "C4 3-GPU rank 1 vs 1 GPU")
+
+
+@pytest.mark.gpu
+def test_c3_fixed_total_8gpu_shard_equals_the_one_gpu_run(engine_mod):
+    """The metric's fixed-total reading (bench.py --scaling strong): the 8-GPU rank-7 shard (131,072 contiguous ids,
+    two waves per SIMD) equals the same ids of the one-GPU run (2^20 replicates, rotation) bit for bit."""
+    ids1, s1 = _rank_summaries(engine_mod, "c3", 1, 0, scaling="strong")
+    ids8, s8 = _rank_summaries(engine_mod, "c3", 8, 7, scaling="strong")
+    assert len(ids1) == 1 << 20 and len(ids8) == 1 << 17
+    _assert_same_replicates(ids1, s1, ids8, s8, "C3 fixed total, 8-GPU rank 7 vs 1 GPU")

@@ -202,20 +202,6 @@ def test_gpu_bin_store_paired_lanes_match_oracle(name, blocks, engine_mod, oracl
     _compare(engine_mod.run(spec, want_rows=True), oracle_mod.run(spec, mode="philox", want_rows=True), name)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("blocks", ["0", "2"])
-@pytest.mark.parametrize("name", sorted(BIN_CASES))
-def test_gpu_bin_store_quads_match_oracle(name, blocks, engine_mod, oracle_mod, monkeypatch):
-    """Quads forced (ECDNA_SSA_PAIR = 3; DESIGN.md §5: lane 4j owns a replicate, lanes 4j + 1 .. 4j + 3 form the
-    Philox blocks and soft logs of its events e + 1 .. e + 3, all four evaluate its state chain) on every bin-store
-    case, bit for bit against the oracle, on the default grid and on two workgroups."""
-    monkeypatch.setenv("ECDNA_SSA_PAIR", "3")
-    if blocks != "0":
-        monkeypatch.setenv("ECDNA_SSA_MAX_BLOCKS", blocks)
-    spec = BIN_CASES[name]
-    _compare(engine_mod.run(spec, want_rows=True), oracle_mod.run(spec, mode="philox", want_rows=True), name)
-
-
 def _no_uneven_small_specs():
     """The no-uneven rule's redraws at small copy numbers (n = 2k <= 32: a draw is rejected with probability
     2^(1-n), so k = 1 cells redraw about once per division and reach the spares and then Philox blocks):
@@ -290,12 +276,6 @@ def test_gpu_nminus_fast_forward_matches_oracle(name, engine_mod, oracle_mod, mo
     monkeypatch.setenv("ECDNA_SSA_PAIR", "1")
     monkeypatch.setenv("ECDNA_SSA_MAX_BLOCKS", "2")
     _compare(engine_mod.run(spec, want_rows=True), cpu, f"{name}/pair-refill")
-    # quads (four events per fast-forward step), on the default grid and refilling on two workgroups
-    monkeypatch.setenv("ECDNA_SSA_PAIR", "3")
-    monkeypatch.delenv("ECDNA_SSA_MAX_BLOCKS")
-    _compare(engine_mod.run(spec, want_rows=True), cpu, f"{name}/quad")
-    monkeypatch.setenv("ECDNA_SSA_MAX_BLOCKS", "2")
-    _compare(engine_mod.run(spec, want_rows=True), cpu, f"{name}/quad-refill")
     s = cpu.summaries
     ev = s["events_by_type"].astype(np.int64)
     nminus_share = (ev[:, 0] + ev[:, 2]).sum() / ev.sum()

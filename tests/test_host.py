@@ -80,6 +80,7 @@ def test_cli_rate_outside_the_engine_range_is_a_usage_error(host, flag, value):
     reference's any-f32 clap values: reported before any GPU work, exit code 2."""
     out = subprocess.run([CLI, "--dry-run", flag, value, "/tmp/ecdna_out"], capture_output=True, text=True)
     assert out.returncode == 2 and "2^-60, 2^60" in out.stderr, out.stderr
+    assert f"invalid value '{value}' for '{flag} <RATE>'" in out.stderr, out.stderr  # the argument as given (ADVICE r05)
     for ok in ("0", "1e-18", "1e18"):
         assert subprocess.run([CLI, "--dry-run", flag, ok, "/tmp/ecdna_out"], capture_output=True).returncode == 0
 

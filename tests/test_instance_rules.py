@@ -39,7 +39,7 @@ BENCH = [
     ("C2 (pure birth: no pairing)", 65_536, {"pair_ok": False}, 1),
     ("C5, 8-GPU shard: half a wave per SIMD, paired", 32_768, {}, 3),
     ("C5, 4-GPU shard: one wave per SIMD", 65_536, {}, 1),
-    ("C5 whole (K = 32 / u32)", 262_144, {}, 1),
+    ("C5 whole (K = 64 / u32: LDS bounds both builds at 2 workgroups per CU)", 262_144, {"occ_def": 2, "occ_ilp": 2}, 1),
     ("C4, 8-GPU shard (K = 64 / u16: default 4, max-ILP 3 workgroups per CU; 2 per lane)", 524_288,
      {"k64u16": True, "occ_def": 4, "occ_ilp": 3}, 1),
     ("C4 whole (16 per lane): the 128-VGPR build", 4_194_304, {"k64u16": True, "occ_def": 4, "occ_ilp": 3}, 2),
@@ -54,8 +54,8 @@ def test_bench_shapes_choose_their_instances(rule, name, n, kw, expect):
 
 
 def test_overrides(rule):
-    assert rule(1 << 20, pair_mode=3) == 4  # quads on request only
-    assert rule(1 << 20, pair_ok=False, pair_mode=3) == 1  # (not without a paired instance)
+    assert rule(1 << 20, pair_mode=3) == 1  # (round 5's quads, ECDNA_SSA_PAIR = 3, are gone: 3 is auto-like, unpaired)
+    assert rule(1 << 20, pair_ok=False, pair_mode=1) == 1  # (no pairs without a paired instance)
     assert rule(32_768, pair_mode=0) == 1  # pairing off
     assert rule(1 << 20, pair_mode=1) == 3  # pairs forced
     assert rule(32_768, sched=0) == 0 and rule(1 << 20, sched=1) == 1
@@ -64,7 +64,7 @@ def test_overrides(rule):
 
 @pytest.mark.parametrize("pair_ok,k64u16,tf0", list(itertools.product([False, True], repeat=3)))
 def test_rule_invariants_over_user_shapes(rule, pair_ok, k64u16, tf0):
-    """auto never picks quads; pairs only with a paired instance and at most half a wave of replicates per SIMD; the
+    """pairs only with a paired instance and at most half a wave of replicates per SIMD; the
     128-VGPR build only for K = 64 / u16 without the runtime-flag variant; one wave per SIMD or less is max-ILP"""
     for n, (od, oi) in itertools.product([1, 100, 32_768, 32_769, 65_536, 65_537, 1 << 20, 1 << 22, 1 << 24],
                                          [(4, 4), (4, 3), (3, 4), (2, 2)]):

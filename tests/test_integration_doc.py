@@ -142,3 +142,30 @@ def test_exported_symbols_are_the_header_entry_points():
     from ecdna_evo_amd import engine
 
     assert set(engine.EXPORTS) == set(header_functions())
+
+
+CLI = os.path.join(REPO, "ecdna-evo_amd", "bin", "ecdna-dynamics")
+
+
+def test_cli_extra_flag_table_matches_help():
+    """the CLI's extra flags (those past the reference's clap interface) are exactly
+    the table's, checked against `ecdna-dynamics --help` both ways, and the `--draws reference` row says what the code
+    does: subsamples continue the replicate's ChaCha8 stream (host/dynamics_main.cpp; src/main.rs:110-123)."""
+    import subprocess
+
+    import pytest
+
+    if not os.path.exists(CLI):
+        pytest.skip("ecdna-dynamics not built")
+    help_text = subprocess.run([CLI, "--help"], capture_output=True, text=True, check=True).stdout
+    # the extras are listed after the reference's last flag (-v, --verbosity) and before -h, --help
+    tail = help_text[help_text.index("--verbosity"):help_text.index("--help")]
+    help_flags = set(re.findall(r"^\s+(--[a-z0-9-]+)", tail, re.M))
+    with open(DOC) as f:
+        doc = f.read()
+    table = doc[doc.index("| flag | meaning |"):]
+    table = table[:table.index("\n\n")]
+    doc_flags = set(re.findall(r"^\| `(--[a-z0-9-]+)", table, re.M))
+    assert doc_flags == help_flags, (sorted(doc_flags - help_flags), sorted(help_flags - doc_flags))
+    ref_row = next(ln for ln in table.splitlines() if ln.startswith("| `--draws"))
+    assert "ChaCha8" in ref_row and "Philox side stream" not in ref_row

@@ -154,3 +154,14 @@ def test_create_process_preserves_state(oracle_mod, distr, _time):
     assert s["iters"] == 0 and s["nplus"] == len(cells) and s["nminus"] == nminus and s["time"] == 0.0
     assert s["stop_reason"] == abi.STOP_MAX_CELLS
     assert np.array_equal(r.row(0), np.asarray(sorted(cells), np.uint16))
+
+
+def test_nplus_events_on_an_empty_nplus_set_return_the_internal_error(oracle_mod):
+    """pick_remove_random_nplus errors on an empty N+ set (src/proliferation.rs:55-57). The oracle's event kernels
+    return ECDNA_REP_ERR_INTERNAL there, the code the engine's guard stops such a replicate with (ABI v11), and leave
+    the distribution unchanged."""
+    d = oracle_mod.Distribution([], 5)
+    rc, _, _, _ = d.increase_nplus(abi.SEG_BINOMIAL, 42, 0, 0)
+    assert rc == abi.REP_ERR_INTERNAL == 5
+    assert d.decrease_nplus(42, 0, 0) == abi.REP_ERR_INTERNAL
+    assert d.nplus == 0 and d.nminus == 5

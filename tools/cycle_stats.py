@@ -1,8 +1,8 @@
 """Loop-section cycle counters of the bin stepper over one launch (development tool): where a wave's time
 goes (replicate boundary, N- fast-forward, full event), per wave-iteration and per event. Needs a library
 built with -DECDNA_CYCLE_STATS (EXTRA=-DECDNA_CYCLE_STATS bash tools/ab_build.sh WORKTREE cyc), selected
-with ECDNA_SSA_LIB. Usage: [PROBE_KMAX=K] python tools/cycle_stats.py [c2|c3|c4|c5|c4k<ex>] (C4 and C5: the 8-GPU rank-0 shard; c4k<ex>:
-its sets of k0 = 2^ex)"""
+with ECDNA_SSA_LIB. Usage: [PROBE_KMAX=K] python tools/cycle_stats.py [c2|c3|c4|c5|c4k<ex>|c3s<G>] (C4 and C5: the 8-GPU rank-0 shard;
+c4k<ex>: its sets of k0 = 2^ex; c3s<G>: the rank-0 shard of C3's fixed total over G GPUs, bench.py --scaling strong)"""
 import ctypes as C
 import dataclasses
 import json
@@ -22,7 +22,14 @@ NAMES = ["cyc_boundary", "cyc_ff", "cyc_full", "iters", "ff_entries", "ff_steps"
 
 def main():
     name = sys.argv[1] if len(sys.argv) > 1 else "c5"
-    if name.startswith("c4k"):  # c4k<ex>: the C4 shard's sets of k0 = 2^ex (probe_configs.c4_subset)
+    if name.startswith("c3s"):  # c3s<G>: bench.py --scaling strong's rank-0 shard at G GPUs
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench
+        from ecdna_evo_amd import shard
+        first, n = shard.shard_range(0, int(name[3:]), 1 << 20)
+        spec = bench.workload_spec(first, n, 1 << 20)
+        name = "c3"
+    elif name.startswith("c4k"):  # c4k<ex>: the C4 shard's sets of k0 = 2^ex (probe_configs.c4_subset)
         spec = probe_configs.c4_subset(int(name[3:]))
     else:
         spec = probe_configs.CONFIGS[name](0, 8) if name in ("c4", "c5") else probe_configs.CONFIGS[name]()

@@ -15,6 +15,11 @@
 #     bench_c3, bench_rows   the metric's line (defaults) and the row store's C3 line
 #     smoke      __graft_entry__.smoke()
 #     bench_c2, bench_c4, bench_c5   the other workloads' bench lines
+#     cyc        loop-section cycle counters (tools/cycle_stats.py) of the configs in CYC (default c3s8,c2,c3) with the
+#                -DECDNA_CYCLE_STATS library LIBS names (EXTRA=-DECDNA_CYCLE_STATS bash tools/ab_build.sh WORKTREE <name>)
+#     inject     the indexing guard under fault injection (tools/inject_check.py) with the library LIBS names
+#                (EXTRA=-DECDNA_INJECT_EMPTY_NPLUS bash tools/ab_build.sh WORKTREE <name>)
+#     pmc_ref    SQ counters (two passes) of one C3 step under the reference's own draws (ssa_stepper_refdraws)
 #   LIBS    prebuilt libraries ecdna-evo_amd/lib_ab/<name>/ (tools/ab_build.sh <ref|WORKTREE> <name>)
 #   TAG     prefix of the outputs under gpurun_out/
 # Usage: STEPS=parity,ab_c3 LIBS="base new" TAG=r05x bash tools/gpu_session.sh
@@ -24,10 +29,12 @@ mkdir -p gpurun_out
 STEPS=${STEPS:-suite,ab_c3,latency}
 LIBS=${LIBS:-}
 TAG=${TAG:-sess}
-export ECDNA_SSA_ABI_ANY=1  # (A/B libraries of an earlier ABI with the same layout)
 L=$PWD/ecdna-evo_amd/lib_ab
 for step in ${STEPS//,/ }; do
   echo "== $step"
+  # (only the A/B steps load prebuilt libraries, which may be of an earlier ABI with the same Params layout; every
+  # other step runs the working tree's library under the ABI check)
+  case $step in ab_c3|latency|pmc|cyc|inject) export ECDNA_SSA_ABI_ANY=1 ;; *) unset ECDNA_SSA_ABI_ANY ;; esac
   case $step in
     suite)
       timeout -k 10 700 python3 -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread \
@@ -75,8 +82,31 @@ for l in sys.stdin:
     c4split)
       timeout -k 10 600 python3 -u tools/c4_split.py > gpurun_out/${TAG}_c4_split.jsonl 2> gpurun_out/${TAG}_c4_split.err
       cut -c1-200 gpurun_out/${TAG}_c4_split.jsonl ;;
+    cyc)
+      for n in $LIBS; do
+        C=${CYC:-c3s8,c2,c3}
+        for cfg in ${C//,/ }; do
+          ECDNA_SSA_LIB=$L/$n/libecdna_ssa.so timeout -k 10 300 python3 tools/cycle_stats.py $cfg | tee -a gpurun_out/${TAG}_cyc.jsonl
+        done
+      done ;;
+    inject)
+      for n in $LIBS; do
+        ECDNA_SSA_LIB=$L/$n/libecdna_ssa.so timeout -k 10 120 python3 tools/inject_check.py | tee -a gpurun_out/${TAG}_inject.jsonl
+      done ;;
+    pmc_ref)
+      O=gpurun_out/${TAG}_pmc_ref; mkdir -p $O
+      timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR \
+        SQ_INSTS_BRANCH SQ_WAVES SQ_BUSY_CYCLES -T --output-format csv -d $O/p1 -o pmc -- python3 bench.py --store rows \
+        --draws reference --steps 1 --warmup 0 --no-cpu-baseline > $O/p1.log 2>&1
+      timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+        SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES -T --output-format csv -d $O/p2 -o pmc -- python3 bench.py --store rows \
+        --draws reference --steps 1 --warmup 0 --no-cpu-baseline > $O/p2.log 2>&1
+      timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $O/p3 -o pmc -- python3 bench.py --store rows \
+        --draws reference --steps 1 --warmup 0 --no-cpu-baseline > $O/p3.log 2>&1
+      timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $O/p4 -o pmc -- python3 bench.py --store rows \
+        --draws reference --steps 1 --warmup 0 --no-cpu-baseline > $O/p4.log 2>&1
+      echo "pmc_ref done" ;;
     prof_bins|prof_rows)
-      unset ECDNA_SSA_ABI_ANY
       bash tools/gpu_profile.sh ${TAG}_${step#prof_} ${step#prof_} ;;
     bench_ref)
       timeout -k 10 600 python3 bench.py --store rows --draws reference > gpurun_out/${TAG}_bench_ref_c3.json \
