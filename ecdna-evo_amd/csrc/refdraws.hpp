@@ -183,8 +183,20 @@ __device__ __forceinline__ double float_1_2(uint64_t bits) {
     b ^= c;                              \
     b = __builtin_rotateleft32(b, 7);
 
+// Ring words per lane (a power of two, >= 32): ECDNA_REF_RING. ECDNA_REF_SYNC_TOPUP: when the wave-uniform top-up
+// runs a refill for some lane, every lane with room for a block takes one too (the wave issues the refill's
+// instructions either way), so later events find fewer lanes short of words.
+#ifndef ECDNA_REF_RING
+#define ECDNA_REF_RING 32u
+#endif
+#ifndef ECDNA_REF_SYNC_TOPUP
+#define ECDNA_REF_SYNC_TOPUP 0
+#endif
+static_assert(ECDNA_REF_RING >= 32u && (ECDNA_REF_RING & (ECDNA_REF_RING - 1u)) == 0u, "ring: a power of two >= 32");
+constexpr uint32_t kRingWords = ECDNA_REF_RING;
+
 // The per-lane generator: key (uniform, 8 words from the host's seed_from_u64), 64-bit block counter and
-// stream, and a ring of two 16-word blocks per lane in LDS ([word][lane]: a wave's accesses hit distinct
+// stream, and a ring of kRingWords / 16 16-word blocks per lane in LDS ([word][lane]: a wave's accesses hit distinct
 // banks). Words come out in stream order whatever the refill timing. Lanes consume words at different
 // rates, so a refill inside next_u32 would run (masked) for the whole wave at nearly every draw site;
 // instead top_up(), called once per event at a wave-uniform point, generates the next block for lanes with
@@ -192,11 +204,18 @@ __device__ __forceinline__ double float_1_2(uint64_t bits) {
 // rejection loops).
 struct ChaCha8 {
     const uint32_t* key;   // 8 words
-    uint32_t* buf;         // LDS, ring word w (0..31) of this lane at buf[w * stride]
+    uint32_t* buf;         // LDS, ring word w (0 .. kRingWords - 1) of this lane at buf[w * stride]
     uint32_t stride;
     uint64_t counter;      // next block
     uint32_t s_lo, s_hi;   // stream
-    uint32_t head, tail;   // words read / generated (tail - head = buffered, 0..32)
+    uint32_t head, tail;   // words read / generated (tail - head = buffered, 0 .. kRingWords)
+#ifdef ECDNA_CYCLE_STATS
+    // (development counters, ssa_refdraws.hip: refills inside an event, Exp1 retries, BTPE and BINV draws)
+    uint32_t dbg[4] = {0u, 0u, 0u, 0u};
+#define ECDNA_REF_DBG(rng, i) ((rng).dbg[i] += 1u)
+#else
+#define ECDNA_REF_DBG(rng, i) ((void)0)
+#endif
 
     __device__ __forceinline__ void reset() {
         counter = 0;
@@ -220,18 +239,27 @@ struct ChaCha8 {
             ECDNA_QR(x[2], x[7], x[8], x[13]);
             ECDNA_QR(x[3], x[4], x[9], x[14]);
         }
-        uint32_t* const dst = buf + (tail & 16u) * stride;
+        uint32_t* const dst = buf + (tail & (kRingWords - 16u)) * stride;
 #pragma unroll
         for (int i = 0; i < 16; ++i) dst[i * stride] = x[i] + in[i];
         counter += 1;
         tail += 16u;
     }
     __device__ __forceinline__ void top_up() {
+#if ECDNA_REF_SYNC_TOPUP
+        if (__ballot(tail - head < 16u) != 0ull) {  // (wave-uniform) some lane is short: every lane with room refills
+            if (tail - head <= kRingWords - 16u) refill();
+        }
+#else
         if (tail - head < 16u) refill();
+#endif
     }
     __device__ __forceinline__ uint32_t next_u32() {
-        if (head == tail) refill();
-        return buf[(head++ & 31u) * stride];
+        if (head == tail) {
+            ECDNA_REF_DBG(*this, 0);
+            refill();
+        }
+        return buf[(head++ & (kRingWords - 1u)) * stride];
     }
     __device__ __forceinline__ uint64_t next_u64() {
         const uint32_t lo = next_u32();
@@ -262,6 +290,7 @@ __device__ __forceinline__ double exp1(ChaCha8& rng, const double* zx, const dou
         const double u = float_1_2(bits) - (1.0 - 0x1p-53);
         const double x = u * zx[i];
         if (x < zx[i + 1]) return x;
+        ECDNA_REF_DBG(rng, 1);
         if (i == 0) return ECDNA_ZIG_EXP_R - log_cr(rng.gen_f64(), clog);
         // (the wedge test against the correctly rounded e^-x, decided by lt_exp_cr's filter; x < R < 22)
         if (lt_exp_cr(zf[i + 1] + (zf[i] - zf[i + 1]) * rng.gen_f64(), -x, cexp)) return x;
@@ -282,6 +311,7 @@ enum { BT_NPQ, BT_M, BT_P1, BT_XM, BT_XL, BT_XR, BT_C, BT_P2, BT_LL, BT_LR, BT_P
 __device__ __forceinline__ uint32_t binomial_half(ChaCha8& rng, uint32_t n, const double* btpe, const double* clog) {
     const double p = 0.5, q = 0.5;
     if ((double)n * p < 10.0) {  // BINV (n <= 18): s = p / q = 1, r0 = q^n = 2^-n exactly
+        ECDNA_REF_DBG(rng, 3);
         const double s = p / q;
         const double a = (double)(n + 1u) * s;
         for (;;) {
@@ -301,6 +331,7 @@ __device__ __forceinline__ uint32_t binomial_half(ChaCha8& rng, uint32_t n, cons
             if (!restart) return x;
         }
     }
+    ECDNA_REF_DBG(rng, 2);
     const int64_t SQUEEZE = 20;
     const double* b = btpe + (uint64_t)(n >> 1) * kBtpeRow;
     const double nd = (double)n, npq = b[BT_NPQ], p1 = b[BT_P1], x_m = b[BT_XM], x_l = b[BT_XL], x_r = b[BT_XR];

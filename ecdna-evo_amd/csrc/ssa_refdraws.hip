@@ -37,9 +37,53 @@ constexpr uint32_t kRefBlock = 256;
 #ifndef ECDNA_REF_MIN_WAVES
 #define ECDNA_REF_MIN_WAVES 1
 #endif
+
+// Development cycle counters of the reference-draws stepper (built with -DECDNA_CYCLE_STATS only;
+// tools/cycle_stats_ref.py), per wave, summed over waves: shader-clock cycles in [0] the replicate boundary (finish +
+// claim), [1] the per-event ChaCha8 top-up, [2] the stop checks and the first-reaction draws (Exp1 per positive
+// channel), [3] the cell pick (gen_range + row read; ProliferateNPlus only), [4] the segregation (BINV / BTPE), [5] the
+// rest of the event (other channels' updates, the row update, the commit); counts, summed over lanes: [8] lane
+// loop iterations, [10] lane refills in the top-up, [11] lane refills inside an event (next_u32 on an empty ring), [12]
+// Exp1 loop trips beyond the first, [13] binomial draws by BTPE, [14] by BINV; per wave (lane 0): [9] iterations whose
+// top-up refilled for some lane; [15] whole-kernel cycles. Marks sit at wave-uniform points
+// (a mark waits for the wave's LDS operations: a rough attribution); lane 0 of each wave flushes.
+#ifdef ECDNA_CYCLE_STATS
+__device__ unsigned long long g_cycle_stats_ref[16];
+#define RCYC_DECL                                                                                              \
+    unsigned long long rcy_[16] = {};                                                                         \
+    const unsigned long long rcy_start_ = clock64();                                                          \
+    unsigned long long rcy_t_ = rcy_start_
+#define RCYC_MARK(i)                                                                                           \
+    do {                                                                                                       \
+        const unsigned long long n_ = clock64();                                                               \
+        rcy_[i] += n_ - rcy_t_;                                                                                \
+        rcy_t_ = n_;                                                                                           \
+    } while (0)
+#define RCYC_ADD(i, v) (rcy_[i] += (unsigned long long)(v))
+#define RCYC_FLUSH()                                                                                           \
+    do {                                                                                                       \
+        rcy_[15] = clock64() - rcy_start_;                                                                     \
+        for (int q = 0; q < 4; ++q) rcy_[11 + q] = rng.dbg[q];                                                 \
+        for (int q = 8; q < 15; ++q)                                                                           \
+            if (q != 9) rcy_[q] = wave_sum_u64(rcy_[q]);  /* (lanes that left the loop early add theirs too) */                                                       \
+        if ((threadIdx.x & 63u) == 0u)                                                                         \
+            for (int q = 0; q < 16; ++q)                                                                       \
+                __hip_atomic_fetch_add(&g_cycle_stats_ref[q], rcy_[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
+    } while (0)
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+#else
+#define RCYC_DECL
+#define RCYC_MARK(i) ((void)0)
+#define RCYC_ADD(i, v) ((void)0)
+#define RCYC_FLUSH() ((void)0)
+#endif
 template <bool BD, int SEG>
 __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_refdraws(const StepperArgs a) {
-    __shared__ uint32_t ccbuf[32 * kRefBlock];
+    __shared__ uint32_t ccbuf[refdraws::kRingWords * kRefBlock];
     __shared__ double zx[257], zf[257], clog[3 * ECDNA_CLOG_N], cexp[128];
     // the sampler tables, staged in LDS (per-lane divergent indices)
     for (uint32_t i = threadIdx.x; i < 257u; i += blockDim.x) {
@@ -54,6 +98,7 @@ __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_re
     constexpr int K = BD ? 4 : 2;
 
     refdraws::ChaCha8 rng;
+    RCYC_DECL;
     rng.key = a.ref_key;
     rng.buf = ccbuf + tid;
     rng.stride = kRefBlock;
@@ -118,6 +163,7 @@ __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_re
                 ch = c;
             }
         }
+        RCYC_MARK(2);
         if (ch < 0) {
             stop = ECDNA_STOP_ABSORBING;
             return;
@@ -154,6 +200,7 @@ __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_re
         } else {  // ProliferateNPlus
             const uint32_t i = (uint32_t)rng.gen_range(np);
             const uint32_t k = row[i];
+            RCYC_MARK(3);
             if (k > 32767u) {  // checked_mul panic (src/proliferation.rs:63-67)
                 err = ECDNA_REP_ERR_OVERFLOW;
                 stop = ECDNA_STOP_ERROR;
@@ -178,6 +225,7 @@ __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_re
                 k1 = refdraws::binomial_half(rng, n, a.ref_btpe, clog);
                 if (k1 == 0u || k1 == n) un = SEG == ECDNA_SEG_BINOMIAL_NO_NMINUS ? 2 : 1;
             }
+            RCYC_MARK(4);
             if (un == 0 && np + 1u > a.cell_cap) {
                 err = ECDNA_REP_ERR_CELL_CAP;
                 stop = ECDNA_STOP_ERROR;
@@ -202,6 +250,7 @@ __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_re
     };
 
     for (;;) {
+        RCYC_ADD(8, 1);
         if (!active) {  // claim the next replicate (and set it up)
             li = atomicAdd(a.head, 1u);
             if (li >= a.n) break;
@@ -238,11 +287,31 @@ __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_re
                 continue;
             }
         }
+        RCYC_MARK(0);
+#ifdef ECDNA_CYCLE_STATS
+        {
+            const bool need = rng.tail - rng.head < 16u;
+            RCYC_ADD(9, __ballot(need) ? 1u : 0u);
+            RCYC_ADD(10, need ? 1u : 0u);
+        }
+#endif
         rng.top_up();  // (one refill site per iteration for the wave; see refdraws::ChaCha8)
+        RCYC_MARK(1);
         event();
+        RCYC_MARK(5);
         if (stop) finish();
     }
+    RCYC_FLUSH();
 }
+
+#ifdef ECDNA_CYCLE_STATS
+// Development: read (and reset) the reference-draws stepper's cycle counters (tools/cycle_stats.py ref)
+extern "C" int ecdna_dev_cycle_stats_ref(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cycle_stats_ref), sizeof(g_cycle_stats_ref)) != hipSuccess) return -1;
+    unsigned long long z[16] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_cycle_stats_ref), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #define ECDNA_REF_SEG(BD)                                                                                    \
     {(const void*)ssa_stepper_refdraws<BD, 0>, (const void*)ssa_stepper_refdraws<BD, 1>,                      \

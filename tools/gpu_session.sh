@@ -19,6 +19,9 @@
 #                -DECDNA_CYCLE_STATS library LIBS names (EXTRA=-DECDNA_CYCLE_STATS bash tools/ab_build.sh WORKTREE <name>)
 #     inject     the indexing guard under fault injection (tools/inject_check.py) with the library LIBS names
 #                (EXTRA=-DECDNA_INJECT_EMPTY_NPLUS bash tools/ab_build.sh WORKTREE <name>)
+#     ab_ref     the reference-draws C3 line with each library of LIBS, interleaved twice (tools/ab_ref.sh)
+#     cyc_ref    section cycle counters of the reference-draws stepper (tools/cycle_stats_ref.py c3) with the
+#                -DECDNA_CYCLE_STATS library LIBS names
 #     pmc_ref    SQ counters (two passes) of one C3 step under the reference's own draws (ssa_stepper_refdraws)
 #   LIBS    prebuilt libraries ecdna-evo_amd/lib_ab/<name>/ (tools/ab_build.sh <ref|WORKTREE> <name>)
 #   TAG     prefix of the outputs under gpurun_out/
@@ -34,7 +37,7 @@ for step in ${STEPS//,/ }; do
   echo "== $step"
   # (only the A/B steps load prebuilt libraries, which may be of an earlier ABI with the same Params layout; every
   # other step runs the working tree's library under the ABI check)
-  case $step in ab_c3|latency|pmc|cyc|inject) export ECDNA_SSA_ABI_ANY=1 ;; *) unset ECDNA_SSA_ABI_ANY ;; esac
+  case $step in ab_c3|latency|pmc|cyc|inject|ab_ref|cyc_ref) export ECDNA_SSA_ABI_ANY=1 ;; *) unset ECDNA_SSA_ABI_ANY ;; esac
   case $step in
     suite)
       timeout -k 10 700 python3 -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread \
@@ -88,6 +91,13 @@ for l in sys.stdin:
         for cfg in ${C//,/ }; do
           ECDNA_SSA_LIB=$L/$n/libecdna_ssa.so timeout -k 10 300 python3 tools/cycle_stats.py $cfg | tee -a gpurun_out/${TAG}_cyc.jsonl
         done
+      done ;;
+    ab_ref)
+      bash tools/ab_ref.sh $LIBS | tee gpurun_out/${TAG}_ab_ref.txt ;;
+    cyc_ref)
+      for n in $LIBS; do
+        ECDNA_SSA_LIB=$L/$n/libecdna_ssa.so timeout -k 10 300 python3 tools/cycle_stats_ref.py c3 | tee -a gpurun_out/${TAG}_cyc_ref.jsonl
+        ECDNA_SSA_LIB=$L/$n/libecdna_ssa.so timeout -k 10 300 python3 tools/cycle_stats_ref.py c2 | tee -a gpurun_out/${TAG}_cyc_ref.jsonl
       done ;;
     inject)
       for n in $LIBS; do
