@@ -183,14 +183,51 @@ __device__ __forceinline__ double float_1_2(uint64_t bits) {
     b ^= c;                              \
     b = __builtin_rotateleft32(b, 7);
 
+// The ChaCha8 block (rand_chacha 0.3.1, 8 rounds) of (key, 64-bit block counter, stream) into 16 LDS words dst[i *
+// stride]: the input words plus the permuted words, as rand_chacha's refill hands them out.
+__device__ __forceinline__ void chacha8_block_to_lds(const uint32_t* key, uint32_t* dst, uint32_t stride, uint64_t counter,
+                                                     uint32_t s_lo, uint32_t s_hi) {
+    const uint32_t in[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                             key[0], key[1], key[2], key[3], key[4], key[5], key[6], key[7],
+                             (uint32_t)counter, (uint32_t)(counter >> 32), s_lo, s_hi};
+    uint32_t x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = in[i];
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+        ECDNA_QR(x[0], x[4], x[8], x[12]);
+        ECDNA_QR(x[1], x[5], x[9], x[13]);
+        ECDNA_QR(x[2], x[6], x[10], x[14]);
+        ECDNA_QR(x[3], x[7], x[11], x[15]);
+        ECDNA_QR(x[0], x[5], x[10], x[15]);
+        ECDNA_QR(x[1], x[6], x[11], x[12]);
+        ECDNA_QR(x[2], x[7], x[8], x[13]);
+        ECDNA_QR(x[3], x[4], x[9], x[14]);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dst[i * stride] = x[i] + in[i];
+}
+
+#ifndef ECDNA_REF_INNER_CALL
+#define ECDNA_REF_INNER_CALL 1
+#endif
+#if ECDNA_REF_INNER_CALL
+__device__ __attribute__((noinline)) void chacha8_block_to_lds_call(const uint32_t* key, uint32_t* dst, uint32_t stride,
+                                                                    uint64_t counter, uint32_t s_lo, uint32_t s_hi) {
+    chacha8_block_to_lds(key, dst, stride, counter, s_lo, s_hi);
+}
+#endif
+
 // Ring words per lane (a power of two, >= 32): ECDNA_REF_RING. ECDNA_REF_SYNC_TOPUP: when the wave-uniform top-up
 // runs a refill for some lane, every lane with room for a block takes one too (the wave issues the refill's
 // instructions either way), so later events find fewer lanes short of words.
+// (C3 reference-draws line, same box: ring 32 1,898 ms; ring 64 1,883; ring 64 with the synchronized top-up 1,700;
+// and the out-of-line inner refill 1,668; profiles/r06c_ab_ref.txt)
 #ifndef ECDNA_REF_RING
-#define ECDNA_REF_RING 32u
+#define ECDNA_REF_RING 64u
 #endif
 #ifndef ECDNA_REF_SYNC_TOPUP
-#define ECDNA_REF_SYNC_TOPUP 0
+#define ECDNA_REF_SYNC_TOPUP 1
 #endif
 static_assert(ECDNA_REF_RING >= 32u && (ECDNA_REF_RING & (ECDNA_REF_RING - 1u)) == 0u, "ring: a power of two >= 32");
 constexpr uint32_t kRingWords = ECDNA_REF_RING;
@@ -221,29 +258,22 @@ struct ChaCha8 {
         counter = 0;
         head = tail = 0;
     }
-    __device__ __forceinline__ void refill() {  // one block into ring words tail .. tail + 15 (mod 32)
-        uint32_t in[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
-                           key[0], key[1], key[2], key[3], key[4], key[5], key[6], key[7],
-                           (uint32_t)counter, (uint32_t)(counter >> 32), s_lo, s_hi};
-        uint32_t x[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) x[i] = in[i];
-#pragma unroll
-        for (int i = 0; i < 8; i += 2) {
-            ECDNA_QR(x[0], x[4], x[8], x[12]);
-            ECDNA_QR(x[1], x[5], x[9], x[13]);
-            ECDNA_QR(x[2], x[6], x[10], x[14]);
-            ECDNA_QR(x[3], x[7], x[11], x[15]);
-            ECDNA_QR(x[0], x[5], x[10], x[15]);
-            ECDNA_QR(x[1], x[6], x[11], x[12]);
-            ECDNA_QR(x[2], x[7], x[8], x[13]);
-            ECDNA_QR(x[3], x[4], x[9], x[14]);
-        }
-        uint32_t* const dst = buf + (tail & (kRingWords - 16u)) * stride;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) dst[i * stride] = x[i] + in[i];
+    __device__ __forceinline__ void refill() {  // one block into ring words tail .. tail + 15 (mod kRingWords)
+        chacha8_block_to_lds(key, buf + (tail & (kRingWords - 16u)) * stride, stride, counter, s_lo, s_hi);
         counter += 1;
         tail += 16u;
+    }
+    // the same from a rare site (an event that outran the top-up): one out-of-line copy of the block function for
+    // every such site (ECDNA_REF_INNER_CALL; inlined at each of them, the kernel carried ~23 copies of its ~400
+    // instructions)
+    __device__ __forceinline__ void refill_rare() {
+#if ECDNA_REF_INNER_CALL
+        chacha8_block_to_lds_call(key, buf + (tail & (kRingWords - 16u)) * stride, stride, counter, s_lo, s_hi);
+        counter += 1;
+        tail += 16u;
+#else
+        refill();
+#endif
     }
     __device__ __forceinline__ void top_up() {
 #if ECDNA_REF_SYNC_TOPUP
@@ -257,7 +287,7 @@ struct ChaCha8 {
     __device__ __forceinline__ uint32_t next_u32() {
         if (head == tail) {
             ECDNA_REF_DBG(*this, 0);
-            refill();
+            refill_rare();
         }
         return buf[(head++ & (kRingWords - 1u)) * stride];
     }
@@ -307,13 +337,28 @@ __device__ __forceinline__ double stirling(double a) {
 constexpr int kBtpeRow = 16;  // doubles per row (128 B)
 enum { BT_NPQ, BT_M, BT_P1, BT_XM, BT_XL, BT_XR, BT_C, BT_P2, BT_LL, BT_LR, BT_P3, BT_P4 };
 
-// rand_distr 0.4.3 Binomial::sample for p = 1/2 (n = 2k even, 2 <= n <= 65534): BINV for n p < 10, else BTPE
-__device__ __forceinline__ uint32_t binomial_half(ChaCha8& rng, uint32_t n, const double* btpe, const double* clog) {
+// BINV's factors for n = 2, 4, ..., 18 (the n p < 10 branch of rand_distr 0.4.3 Binomial with p = 1/2): row n / 2 - 1,
+// entry x = 1 .. 110 holds a / x - s with a = (n + 1) s, s = p / q = 1, formed by the same IEEE operations (a correctly
+// rounded f64 division, then the subtraction) as the loop that uses them, so a lookup gives the loop's own value bit for
+// bit (binv_factors stages the table in LDS; the loop's divisions were on its serial chain, ~10 f64 instructions each)
+constexpr int kBinvRows = 9, kBinvCols = 111;
+__device__ __forceinline__ void binv_factors(double* tab, uint32_t tid, uint32_t nthreads) {
+    for (uint32_t i = tid; i < (uint32_t)(kBinvRows * kBinvCols); i += nthreads) {
+        const uint32_t n = 2u * (i / kBinvCols + 1u), x = i % kBinvCols;
+        const double s = 0.5 / 0.5;
+        const double a = (double)(n + 1u) * s;
+        tab[i] = x ? a / (double)x - s : 0.0;
+    }
+}
+
+// rand_distr 0.4.3 Binomial::sample for p = 1/2 (n = 2k even, 2 <= n <= 65534): BINV for n p < 10, else BTPE.
+// binv: the binv_factors table.
+__device__ __forceinline__ uint32_t binomial_half(ChaCha8& rng, uint32_t n, const double* btpe, const double* clog,
+                                                  const double* binv) {
     const double p = 0.5, q = 0.5;
     if ((double)n * p < 10.0) {  // BINV (n <= 18): s = p / q = 1, r0 = q^n = 2^-n exactly
         ECDNA_REF_DBG(rng, 3);
-        const double s = p / q;
-        const double a = (double)(n + 1u) * s;
+        const double* const fac = binv + (n / 2u - 1u) * kBinvCols;  // a / x - s for x = 1 .. 110
         for (;;) {
             double r = __builtin_ldexp(1.0, -(int)n);
             double u = rng.gen_f64();
@@ -326,7 +371,7 @@ __device__ __forceinline__ uint32_t binomial_half(ChaCha8& rng, uint32_t n, cons
                     restart = true;
                     break;
                 }
-                r *= a / (double)x - s;
+                r *= fac[x];
             }
             if (!restart) return x;
         }

@@ -44,31 +44,43 @@ constexpr uint32_t kRefBlock = 256;
 // channel), [3] the cell pick (gen_range + row read; ProliferateNPlus only), [4] the segregation (BINV / BTPE), [5] the
 // rest of the event (other channels' updates, the row update, the commit); counts, summed over lanes: [8] lane
 // loop iterations, [10] lane refills in the top-up, [11] lane refills inside an event (next_u32 on an empty ring), [12]
-// Exp1 loop trips beyond the first, [13] binomial draws by BTPE, [14] by BINV; per wave (lane 0): [9] iterations whose
-// top-up refilled for some lane; [15] whole-kernel cycles. Marks sit at wave-uniform points
-// (a mark waits for the wave's LDS operations: a rough attribution); lane 0 of each wave flushes.
+// Exp1 loop trips beyond the first, [13] binomial draws by BTPE, [14] by BINV; [9] wave-iterations (per wave); [15]
+// whole-kernel cycles (per wave). The cycle attribution is per WAVE: a mark, executed by the wave whenever any lane is
+// active (also inside divergent branches), charges the time since the wave's previous mark to its region, through a
+// per-wave clock in LDS that the wave's first active lane keeps (a mark waits for the wave's LDS operations: a rough
+// attribution of latency, an exact one of the wave's serial time).
 #ifdef ECDNA_CYCLE_STATS
 __device__ unsigned long long g_cycle_stats_ref[16];
 #define RCYC_DECL                                                                                              \
+    __shared__ unsigned long long rcyc_w_[kRefBlock / 64][8];                                                 \
     unsigned long long rcy_[16] = {};                                                                         \
     const unsigned long long rcy_start_ = clock64();                                                          \
-    unsigned long long rcy_t_ = rcy_start_
+    const uint32_t rcy_wave_ = threadIdx.x >> 6;                                                              \
+    if ((threadIdx.x & 63u) == 0u) {                                                                          \
+        for (int q = 0; q < 7; ++q) rcyc_w_[rcy_wave_][q] = 0ull;                                             \
+        rcyc_w_[rcy_wave_][7] = rcy_start_;                                                                   \
+    }
 #define RCYC_MARK(i)                                                                                           \
     do {                                                                                                       \
         const unsigned long long n_ = clock64();                                                               \
-        rcy_[i] += n_ - rcy_t_;                                                                                \
-        rcy_t_ = n_;                                                                                           \
+        const uint32_t l_ = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));                \
+        if (l_ == (uint32_t)__builtin_amdgcn_readfirstlane(l_)) {                                             \
+            rcyc_w_[rcy_wave_][i] += n_ - rcyc_w_[rcy_wave_][7];                                              \
+            rcyc_w_[rcy_wave_][7] = n_;                                                                       \
+        }                                                                                                      \
     } while (0)
 #define RCYC_ADD(i, v) (rcy_[i] += (unsigned long long)(v))
 #define RCYC_FLUSH()                                                                                           \
     do {                                                                                                       \
-        rcy_[15] = clock64() - rcy_start_;                                                                     \
+        __builtin_amdgcn_s_waitcnt(0xc07f);                                                                    \
         for (int q = 0; q < 4; ++q) rcy_[11 + q] = rng.dbg[q];                                                 \
-        for (int q = 8; q < 15; ++q)                                                                           \
-            if (q != 9) rcy_[q] = wave_sum_u64(rcy_[q]);  /* (lanes that left the loop early add theirs too) */                                                       \
-        if ((threadIdx.x & 63u) == 0u)                                                                         \
+        for (int q = 8; q < 15; ++q) rcy_[q] = wave_sum_u64(rcy_[q]);                                          \
+        if ((threadIdx.x & 63u) == 0u) {                                                                       \
+            for (int q = 0; q < 7; ++q) rcy_[q] = rcyc_w_[rcy_wave_][q];                                       \
+            rcy_[15] = clock64() - rcy_start_;                                                                 \
             for (int q = 0; q < 16; ++q)                                                                       \
                 __hip_atomic_fetch_add(&g_cycle_stats_ref[q], rcy_[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
+        }                                                                                                      \
     } while (0)
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long x) {
 #pragma unroll
@@ -85,6 +97,7 @@ template <bool BD, int SEG>
 __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_refdraws(const StepperArgs a) {
     __shared__ uint32_t ccbuf[refdraws::kRingWords * kRefBlock];
     __shared__ double zx[257], zf[257], clog[3 * ECDNA_CLOG_N], cexp[128];
+    __shared__ double binv[refdraws::kBinvRows * refdraws::kBinvCols];
     // the sampler tables, staged in LDS (per-lane divergent indices)
     for (uint32_t i = threadIdx.x; i < 257u; i += blockDim.x) {
         zx[i] = kZigX[i];
@@ -92,6 +105,7 @@ __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_re
     }
     for (uint32_t i = threadIdx.x; i < 3u * ECDNA_CLOG_N; i += blockDim.x) clog[i] = kCLog[i];
     for (uint32_t i = threadIdx.x; i < 128u; i += blockDim.x) cexp[i] = kCExp[i];
+    refdraws::binv_factors(binv, threadIdx.x, blockDim.x);
     __syncthreads();
     const uint32_t tid = threadIdx.x;
     const bool hash_on = (a.flags & ECDNA_FLAG_EVENT_HASH) != 0;
@@ -111,6 +125,12 @@ __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_re
     uint16_t* row = a.rows;
     float rates[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     uint32_t np = 0, nm = 0;
+    // the row's last cell (row[np - 1]), cached: swap_remove reads it at every N+ event, and a read straight from HBM
+    // sat on the event's chain (round 6: the cycle counters put ~40 % of a C3 wave's time after the segregation). A
+    // division pushes its daughters, so the new tail is known; after a death it is reloaded at the top of the next
+    // event, where the load's latency hides behind the first-reaction draws. The row in HBM stays complete.
+    uint32_t tail = 0;
+    bool tail_ok = false;
     uint64_t h = kFnv0;
     float t = 0.0f;
     uint32_t e = 0, stop = 0, err = 0, sj = 0, uneven_n = 0;
@@ -147,6 +167,10 @@ __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_re
         if (t >= a.max_time32) {
             stop = ECDNA_STOP_MAX_TIME;
             return;
+        }
+        if (!tail_ok && np > 0) {  // (after a death, or at the replicate's start)
+            tail = row[np - 1];
+            tail_ok = true;
         }
         // first-reaction method, channel order [PN-, PN+, DN-, DN+]
         const uint32_t pop[4] = {nm, np, nm, np};
@@ -194,12 +218,13 @@ __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_re
             nm -= 1;
         } else if (ch == ECDNA_EV_DEATH_NPLUS) {
             const uint32_t i = (uint32_t)rng.gen_range(np);
-            row[i] = row[np - 1];
+            if (i != np - 1) row[i] = (uint16_t)tail;  // swap_remove(i)
             np -= 1;
+            tail_ok = false;
             x |= (uint64_t)i << 20;
         } else {  // ProliferateNPlus
             const uint32_t i = (uint32_t)rng.gen_range(np);
-            const uint32_t k = row[i];
+            const uint32_t k = i == np - 1 ? tail : row[i];
             RCYC_MARK(3);
             if (k > 32767u) {  // checked_mul panic (src/proliferation.rs:63-67)
                 err = ECDNA_REP_ERR_OVERFLOW;
@@ -214,7 +239,7 @@ __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_re
             } else if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN) {
                 int tries = 0;
                 do {
-                    k1 = refdraws::binomial_half(rng, n, a.ref_btpe, clog);
+                    k1 = refdraws::binomial_half(rng, n, a.ref_btpe, clog, binv);
                 } while ((k1 == 0u || k1 == n) && ++tries < 4096);
                 if (k1 == 0u || k1 == n) {
                     err = ECDNA_REP_ERR_REJECTION;
@@ -222,7 +247,7 @@ __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_re
                     return;
                 }
             } else {
-                k1 = refdraws::binomial_half(rng, n, a.ref_btpe, clog);
+                k1 = refdraws::binomial_half(rng, n, a.ref_btpe, clog, binv);
                 if (k1 == 0u || k1 == n) un = SEG == ECDNA_SEG_BINOMIAL_NO_NMINUS ? 2 : 1;
             }
             RCYC_MARK(4);
@@ -231,14 +256,16 @@ __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_re
                 stop = ECDNA_STOP_ERROR;
                 return;
             }
-            row[i] = row[np - 1];  // pick_remove_random_nplus: swap_remove(i)
+            if (i != np - 1) row[i] = (uint16_t)tail;  // pick_remove_random_nplus: swap_remove(i)
             np -= 1;
             if (un == 0) {
                 row[np++] = (uint16_t)k1;
                 row[np++] = (uint16_t)(n - k1);
+                tail = n - k1;
             } else {
                 if (un == 1) nm += 1;
                 row[np++] = (uint16_t)n;
+                tail = n;
                 uneven_n += 1;
             }
             x |= ((uint64_t)k1 << 2) | ((uint64_t)i << 20);
@@ -270,6 +297,7 @@ __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_re
             }
             for (uint32_t j = 0; j < np; ++j) row[j] = src[j];
             nm = (uint32_t)(a.init_nminus_set ? a.init_nminus_set[set] : a.init_nminus);
+            tail_ok = false;
             const uint64_t stream = a.seed * 10ull + rid;  // src/main.rs:56-58
             rng.reset();
             rng.s_lo = (uint32_t)stream;
@@ -291,7 +319,8 @@ __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_re
 #ifdef ECDNA_CYCLE_STATS
         {
             const bool need = rng.tail - rng.head < 16u;
-            RCYC_ADD(9, __ballot(need) ? 1u : 0u);
+            const uint32_t l_ = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+            RCYC_ADD(9, l_ == (uint32_t)__builtin_amdgcn_readfirstlane(l_) ? 1u : 0u);  // (summed over lanes: per wave)
             RCYC_ADD(10, need ? 1u : 0u);
         }
 #endif
