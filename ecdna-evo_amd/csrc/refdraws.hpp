@@ -99,6 +99,37 @@ __device__ __forceinline__ double log_cr(double x, const double* clog) {
     return s.hi + s.lo;
 }
 
+// ln x for x in (0, 1) in plain double arithmetic (log_cr's reduction and table head, a degree-7 polynomial in r,
+// |r| <= 2^-8): within 2^-45 of ln x, absolute (|ln x| <= 37 here, so e ln 2 and the final sum carry the largest
+// roundings, 2^-47 each). Not correctly rounded: only used to decide integer truncations clear of their boundary
+// (trunc_log_ratio), as exp_approx decides lt_exp_cr.
+__device__ __forceinline__ double log_approx(double x, const double* clog) {
+    const uint64_t u = (uint64_t)__double_as_longlong(x);
+    int64_t e = (int64_t)(u >> 52) - 1023;
+    double f = __longlong_as_double((long long)((u & 0x000fffffffffffffull) | 0x3ff0000000000000ull));
+    if (f >= 1.41796875) {
+        f = f * 0.5;
+        e += 1;
+    }
+    const int j = (int)(f * 128.0 + 0.5);
+    const double* t = clog + 3 * (j - ECDNA_CLOG_J0);
+    const double r = __builtin_fma(f, t[0], -1.0);
+    double q = __builtin_fma(r, -1.0 / 7.0, 1.0 / 6.0);  // (signs folded: ln(1 + r) = r - r^2 (1/2 - r (1/3 - ...)))
+    q = __builtin_fma(r, -q, 1.0 / 5.0);
+    q = __builtin_fma(r, -q, 1.0 / 4.0);
+    q = __builtin_fma(r, -q, 1.0 / 3.0);
+    q = __builtin_fma(r, -q, 1.0 / 2.0);
+    const double l1p = __builtin_fma(-r * r, q, r);
+    return __builtin_fma((double)e, ECDNA_CLN2_HI, t[1] + l1p);
+}
+
+// f64_to_i64(base + sign * log_cr(v) / lambda), BTPE's region 3 (sign = +1) and region 4 (sign = -1) step, decided
+// with log_approx wherever the quotient's truncation is clear of an integer boundary by 2^-30 (the approximation and
+// the exact path differ by at most ~2^-45 / lambda + a few ulp of the sum: lambda >= 2^-7 for n <= 65534), else with
+// the correctly rounded log: the exact path's value, bit for bit, without its double-double polynomial (~150 f64
+// instructions) on the common path. v == 0 (probability 2^-52) takes the exact path.
+__device__ __forceinline__ int64_t trunc_log_ratio(double base, double sign, double v, double lambda, const double* clog);
+
 // e^y, correctly rounded for |y| <= 22 (oracle_compat_exp: the same operations). cexp: {hi, lo} of 2^(j/64).
 __device__ __forceinline__ double exp_cr(double y, const double* cexp) {
     if (y != y) return y;
@@ -161,6 +192,15 @@ __device__ __forceinline__ int64_t f64_to_i64(double x) {
     if (x >= 0x1p63) return INT64_MAX;
     if (x < -0x1p63) return INT64_MIN;
     return (int64_t)x;
+}
+
+__device__ __forceinline__ int64_t trunc_log_ratio(double base, double sign, double v, double lambda, const double* clog) {
+    if (v > 0.0) {
+        const double ta = base + sign * (log_approx(v, clog) / lambda);
+        const double d = ta - __builtin_rint(ta);
+        if (__builtin_fabs(d) > 0x1p-30 && __builtin_fabs(ta) < 0x1p52) return (int64_t)ta;
+    }
+    return f64_to_i64(base + sign * (log_cr(v, clog) / lambda));
 }
 
 // bits >> 12 as the mantissa of a value in [1, 2) (rand's into_float_with_exponent(0))
@@ -353,10 +393,11 @@ __device__ __forceinline__ void binv_factors(double* tab, uint32_t tid, uint32_t
 
 // rand_distr 0.4.3 Binomial::sample for p = 1/2 (n = 2k even, 2 <= n <= 65534): BINV for n p < 10, else BTPE.
 // binv: the binv_factors table.
-__device__ __forceinline__ uint32_t binomial_half(ChaCha8& rng, uint32_t n, const double* btpe, const double* clog,
-                                                  const double* binv) {
-    const double p = 0.5, q = 0.5;
-    if ((double)n * p < 10.0) {  // BINV (n <= 18): s = p / q = 1, r0 = q^n = 2^-n exactly
+__device__ __forceinline__ bool binomial_half_is_binv(uint32_t n) { return (double)n * 0.5 < 10.0; }
+
+// BINV (n p < 10, n <= 18): s = p / q = 1, r0 = q^n = 2^-n exactly
+__device__ __forceinline__ uint32_t binv_half(ChaCha8& rng, uint32_t n, const double* binv) {
+    {
         ECDNA_REF_DBG(rng, 3);
         const double* const fac = binv + (n / 2u - 1u) * kBinvCols;  // a / x - s for x = 1 .. 110
         for (;;) {
@@ -376,6 +417,11 @@ __device__ __forceinline__ uint32_t binomial_half(ChaCha8& rng, uint32_t n, cons
             if (!restart) return x;
         }
     }
+}
+
+// BTPE (n p >= 10)
+__device__ __forceinline__ uint32_t btpe_half(ChaCha8& rng, uint32_t n, const double* btpe, const double* clog) {
+    const double p = 0.5, q = 0.5;
     ECDNA_REF_DBG(rng, 2);
     const int64_t SQUEEZE = 20;
     const double* b = btpe + (uint64_t)(n >> 1) * kBtpeRow;
@@ -396,11 +442,11 @@ __device__ __forceinline__ uint32_t binomial_half(ChaCha8& rng, uint32_t n, cons
             if (v > 1.) continue;
             y = f64_to_i64(x);
         } else if (!(u > p3)) {
-            y = f64_to_i64(x_l + log_cr(v, clog) / lambda_l);
+            y = trunc_log_ratio(x_l, 1.0, v, lambda_l, clog);  // f64_to_i64(x_l + log_cr(v) / lambda_l)
             if (y < 0) continue;
             v *= (u - p2) * lambda_l;
         } else {
-            y = f64_to_i64(x_r - log_cr(v, clog) / lambda_r);
+            y = trunc_log_ratio(x_r, -1.0, v, lambda_r, clog);  // f64_to_i64(x_r - log_cr(v) / lambda_r)
             if (y > 0 && (uint64_t)y > (uint64_t)n) continue;
             v *= (u - p3) * lambda_r;
         }
@@ -408,6 +454,21 @@ __device__ __forceinline__ uint32_t binomial_half(ChaCha8& rng, uint32_t n, cons
         if (!(k > SQUEEZE && (double)k < 0.5 * npq - 1.)) {
             const double s = p / q;
             const double a = s * (nd + 1.);
+            // (filter) f is the ratio C(n, y) / C(n, m) = prod (n + 1 - i) / i over i in (m, y] (or its inverse for
+            // y < m), formed below by one f64 division per factor. For k <= 20 the decision v > f is taken first
+            // from that ratio as one quotient of two products of exact integers (within ~2^-47 of the real ratio,
+            // as is the loop's f: 3 roundings per factor), wherever v is clear of it by 2^-40 relative; else by
+            // the loop's own f. Same decision bit for bit, without ~20 f64 divisions on the common path.
+            if (k <= 20) {
+                double num = 1.0, den = 1.0;
+                for (int64_t i = (m < y ? m : y) + 1; i <= (m < y ? y : m); ++i) {
+                    num *= nd + 1. - (double)i;
+                    den *= (double)i;
+                }
+                const double fa = m < y ? num / den : (m > y ? den / num : 1.0);
+                if (v > fa * (1.0 + 0x1p-40)) continue;
+                if (v < fa * (1.0 - 0x1p-40)) break;
+            }
             double f = 1.0;
             if (m < y) {
                 int64_t i = m;
@@ -442,6 +503,11 @@ __device__ __forceinline__ uint32_t binomial_half(ChaCha8& rng, uint32_t n, cons
         break;
     }
     return (uint32_t)y;
+}
+
+__device__ __forceinline__ uint32_t binomial_half(ChaCha8& rng, uint32_t n, const double* btpe, const double* clog,
+                                                  const double* binv) {
+    return binomial_half_is_binv(n) ? binv_half(rng, n, binv) : btpe_half(rng, n, btpe, clog);
 }
 
 }  // namespace refdraws

@@ -41,8 +41,8 @@ constexpr uint32_t kRefBlock = 256;
 // Development cycle counters of the reference-draws stepper (built with -DECDNA_CYCLE_STATS only;
 // tools/cycle_stats_ref.py), per wave, summed over waves: shader-clock cycles in [0] the replicate boundary (finish +
 // claim), [1] the per-event ChaCha8 top-up, [2] the stop checks and the first-reaction draws (Exp1 per positive
-// channel), [3] the cell pick (gen_range + row read; ProliferateNPlus only), [4] the segregation (BINV / BTPE), [5] the
-// rest of the event (other channels' updates, the row update, the commit); counts, summed over lanes: [8] lane
+// channel), [3] the cell pick (gen_range + row read; ProliferateNPlus only), [4] the segregation (BTPE under the Binomial
+// rules; all of it under the others), [6] BINV (the Binomial rules), [5] the rest of the event (other channels' updates, the row update, the commit); counts, summed over lanes: [8] lane
 // loop iterations, [10] lane refills in the top-up, [11] lane refills inside an event (next_u32 on an empty ring), [12]
 // Exp1 loop trips beyond the first, [13] binomial draws by BTPE, [14] by BINV; [9] wave-iterations (per wave); [15]
 // whole-kernel cycles (per wave). The cycle attribution is per WAVE: a mark, executed by the wave whenever any lane is
@@ -247,7 +247,14 @@ __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_re
                     return;
                 }
             } else {
+#ifdef ECDNA_CYCLE_STATS  // (the two samplers as separate regions: [6] BINV, [4] BTPE)
+                const bool binv_n = refdraws::binomial_half_is_binv(n);
+                if (binv_n) k1 = refdraws::binv_half(rng, n, binv);
+                RCYC_MARK(6);
+                if (!binv_n) k1 = refdraws::btpe_half(rng, n, a.ref_btpe, clog);
+#else
                 k1 = refdraws::binomial_half(rng, n, a.ref_btpe, clog, binv);
+#endif
                 if (k1 == 0u || k1 == n) un = SEG == ECDNA_SEG_BINOMIAL_NO_NMINUS ? 2 : 1;
             }
             RCYC_MARK(4);

@@ -17,7 +17,7 @@ from ecdna_evo_amd import abi, engine  # noqa: E402
 
 import bench  # noqa: E402
 
-NAMES = ["cyc_boundary", "cyc_topup", "cyc_first_reaction", "cyc_pick", "cyc_segregation", "cyc_rest", "", "",
+NAMES = ["cyc_boundary", "cyc_topup", "cyc_first_reaction", "cyc_pick", "cyc_btpe", "cyc_rest", "cyc_binv", "",
          "lane_iters", "wave_iters_refilled", "lane_refills_topup", "lane_refills_inner", "exp1_retries",
          "btpe_draws", "binv_draws", "cyc_kernel"]
 
@@ -42,7 +42,7 @@ def main():
     geo = ctx.geometry()
     ctx.close()
     waves = geo[1] // 64
-    sec = [k for k in NAMES[:6]]
+    sec = [k for k in NAMES[:7]]
     tot = sum(d[k] for k in sec)
     print(json.dumps({"config": f"{wl} reference draws", "replicates": n, "ms": ms, "events": ev, "events_per_s": ev / ms * 1e3,
                       "grid_lanes": geo[1], **d,

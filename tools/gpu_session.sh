@@ -22,6 +22,8 @@
 #     ab_ref     the reference-draws C3 line with each library of LIBS, interleaved twice (tools/ab_ref.sh)
 #     cyc_ref    section cycle counters of the reference-draws stepper (tools/cycle_stats_ref.py c3) with the
 #                -DECDNA_CYCLE_STATS library LIBS names
+#     c5curve    the C5 rank-0 shards of 8, 4 and 2 GPUs and the whole run (G = 1) at K = 64, one after another
+#                (tools/probe_configs.py c5): the same-K strong-scaling curve
 #     pmc_ref    SQ counters (two passes) of one C3 step under the reference's own draws (ssa_stepper_refdraws)
 #   LIBS    prebuilt libraries ecdna-evo_amd/lib_ab/<name>/ (tools/ab_build.sh <ref|WORKTREE> <name>)
 #   TAG     prefix of the outputs under gpurun_out/
@@ -98,6 +100,11 @@ for l in sys.stdin:
       for n in $LIBS; do
         ECDNA_SSA_LIB=$L/$n/libecdna_ssa.so timeout -k 10 300 python3 tools/cycle_stats_ref.py c3 | tee -a gpurun_out/${TAG}_cyc_ref.jsonl
         ECDNA_SSA_LIB=$L/$n/libecdna_ssa.so timeout -k 10 300 python3 tools/cycle_stats_ref.py c2 | tee -a gpurun_out/${TAG}_cyc_ref.jsonl
+      done ;;
+    c5curve)
+      for G in 8 4 2 1; do
+        PROBE_FLAGS=0x20 PROBE_KMAX=64 PROBE_GPUS=$G timeout -k 10 200 python3 tools/probe_configs.py c5 2>/dev/null | \
+          python3 -c "import json,sys; d=json.loads(sys.stdin.read()); i=d['instance']; print('c5 G=$G rank0', round(d['stepper_ms'],1), 'ms', 'replicates', d['replicates'], 'events', d['events'], 'K', i['bin_kmax'], 'paired', i['paired'], 'schedule', i['schedule'], 'errors', d['errors'])" | tee -a gpurun_out/${TAG}_c5curve.txt
       done ;;
     inject)
       for n in $LIBS; do
