@@ -97,6 +97,8 @@ def lib():
     L.oracle_compat_exp.restype = C.c_double
     L.oracle_compat_exp_approx.argtypes = [C.c_double]
     L.oracle_compat_exp_approx.restype = C.c_double
+    L.oracle_compat_log_approx.argtypes = [C.c_double]
+    L.oracle_compat_log_approx.restype = C.c_double
     _lib = L
     return L
 
@@ -275,6 +277,11 @@ def compat_exp(x: float) -> float:
 def compat_exp_approx(x: float) -> float:
     """csrc/refdraws.hpp exp_approx restated (the wedge-test filter; tests only)."""
     return lib().oracle_compat_exp_approx(x)
+
+
+def compat_log_approx(x: float) -> float:
+    """csrc/refdraws.hpp log_approx restated (BTPE's region-3/4 filter; tests only)."""
+    return lib().oracle_compat_log_approx(x)
 
 
 def chacha_block(state, rounds: int):

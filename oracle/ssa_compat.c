@@ -356,6 +356,29 @@ double oracle_compat_exp_approx(double y) {
     return ldexp(CEXP_TAB[2 * jj] * q, (int)qq);
 }
 
+/* csrc/refdraws.hpp log_approx, the same operations: the GPU's plain-double ln x (0 < x < 1) that decides BTPE's
+ * region-3/4 truncations clear of an integer boundary (trunc_log_ratio); restated here so that a CPU test can bound
+ * its error against exact arithmetic (tests/test_compat_math.py). The compat draws never use it. */
+double oracle_compat_log_approx(double x) {
+    const uint64_t u = d2u(x);
+    int64_t e = (int64_t)(u >> 52) - 1023;
+    double f = u2d((u & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
+    if (f >= 1.41796875) {
+        f = f * 0.5;
+        e += 1;
+    }
+    const int j = (int)(f * 128.0 + 0.5);
+    const double* t = CLOG_TAB + 3 * (j - ECDNA_CLOG_J0);
+    const double r = fma(f, t[0], -1.0);
+    double q = fma(r, -1.0 / 7.0, 1.0 / 6.0);
+    q = fma(r, -q, 1.0 / 5.0);
+    q = fma(r, -q, 1.0 / 4.0);
+    q = fma(r, -q, 1.0 / 3.0);
+    q = fma(r, -q, 1.0 / 2.0);
+    const double l1p = fma(-r * r, q, r);
+    return fma((double)e, ECDNA_CLN2_HI, t[1] + l1p);
+}
+
 /* Rust's `f as i64`: saturating, NaN -> 0 (a C cast of an out-of-range double is undefined) */
 static inline int64_t f64_to_i64(double x) {
     if (x != x) return 0;

@@ -71,6 +71,57 @@ def test_exp_filter_error_bound(oracle_mod):
     assert worst < 2.0 ** -48, worst
 
 
+def test_log_filter_error_bound(oracle_mod):
+    """BTPE's region-3/4 step truncates x +- ln(v) / lambda (csrc/refdraws.hpp trunc_log_ratio) from a plain-double
+    ln v wherever the result is clear of an integer by 2^-30; exact provided log_approx is within ~2^-38 lambda of
+    ln v (lambda >= 2^-7). Its restatement is within 2^-45 (absolute) over BTPE's inputs v in [2^-52, 1) (multiples of
+    2^-52: float_1_2(bits) - 1), the smallest and the values next to 1 included."""
+    getcontext().prec = 60
+    rng = random.Random(13)
+    vs = [rng.randrange(1, 1 << 52) * 2.0 ** -52 for _ in range(6000)]
+    vs += [rng.randrange(1, 1 << 20) * 2.0 ** -52 for _ in range(1000)]  # far tail
+    vs += [2.0 ** -52, 1.0 - 2.0 ** -52, 0.5, 0.5 - 2.0 ** -52, 0.70898, 0.708984375, 0.99, 2.0 ** -26]
+    worst = 0.0
+    for v in vs:
+        err = abs(Decimal(oracle_mod.compat_log_approx(v)) - Decimal(v).ln())
+        worst = max(worst, float(err))
+    assert worst < 2.0 ** -45, worst
+
+
+@pytest.mark.parametrize("n", [20, 22, 24, 30, 40, 41 * 2, 64, 128, 256, 1000, 4096, 65534])
+def test_btpe_explicit_ratio_filter_error_bound(n):
+    """BTPE's explicit acceptance v > f (k = |y - m| <= 20; csrc/refdraws.hpp) is decided first from
+    fa = prod(n + 1 - i) / prod(i) (or its inverse) wherever v is clear of it by 2^-40 relative: exact provided fa and
+    the loop's f (f *= a / i - s per factor, f /= ... for y < m; the reference's operations, restated with Python's
+    IEEE doubles) are each within 2^-41 of the real ratio C(n, y) / C(n, m). Both are, for every y with |y - m| <= 20
+    in [0, n] and the BTPE m of Binomial(n, 1/2)."""
+    from fractions import Fraction
+
+    p = q = 0.5
+    s = p / q
+    a = s * (n + 1.0)
+    m = int(n * p + p)  # (f_m = n p + p, m = f_m as i64)
+    worst_f, worst_fa = 0.0, 0.0
+    for y in range(max(0, m - 20), min(n, m + 20) + 1):
+        f, num, den = 1.0, 1.0, 1.0
+        exact = Fraction(1)
+        lo, hi = (m, y) if m < y else (y, m)
+        for i in range(lo + 1, hi + 1):
+            if m < y:
+                f *= a / float(i) - s
+            else:
+                f /= a / float(i) - s
+            num *= n + 1.0 - float(i)
+            den *= float(i)
+            exact *= Fraction(n + 1 - i, i)
+        if m > y:
+            exact = 1 / exact
+        fa = num / den if m < y else (den / num if m > y else 1.0)
+        worst_f = max(worst_f, abs(float((Fraction(f) - exact) / exact)))
+        worst_fa = max(worst_fa, abs(float((Fraction(fa) - exact) / exact)))
+    assert worst_f < 2.0 ** -41 and worst_fa < 2.0 ** -41, (worst_f, worst_fa)
+
+
 @pytest.mark.parametrize("fn,gen", [
     ("log", lambda r: r.random() or 0.5),
     ("log", lambda r: r.uniform(0.5, 3.0)),
