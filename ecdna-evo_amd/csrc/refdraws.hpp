@@ -124,11 +124,12 @@ __device__ __forceinline__ double log_approx(double x, const double* clog) {
 }
 
 // f64_to_i64(base + sign * log_cr(v) / lambda), BTPE's region 3 (sign = +1) and region 4 (sign = -1) step, decided
-// with log_approx wherever the quotient's truncation is clear of an integer boundary by 2^-30 (the approximation and
-// the exact path differ by at most ~2^-45 / lambda + a few ulp of the sum: lambda >= 2^-7 for n <= 65534), else with
-// the correctly rounded log: the exact path's value, bit for bit, without its double-double polynomial (~150 f64
+// with log_approx times inv_lambda = RN(1 / lambda) wherever the result's truncation is clear of an integer boundary by
+// 2^-30 (the approximation and the exact path differ by at most ~2^-45 / lambda + a few ulp of the product and the sum:
+// lambda >= 2^-7 for n <= 65534), else with the correctly rounded log and the division: the exact path's value, bit for bit, without its double-double polynomial (~150 f64
 // instructions) on the common path. v == 0 (probability 2^-52) takes the exact path.
-__device__ __forceinline__ int64_t trunc_log_ratio(double base, double sign, double v, double lambda, const double* clog);
+__device__ __forceinline__ int64_t trunc_log_ratio(double base, double sign, double v, double lambda, double inv_lambda,
+                                                   const double* clog);
 
 // e^y, correctly rounded for |y| <= 22 (oracle_compat_exp: the same operations). cexp: {hi, lo} of 2^(j/64).
 __device__ __forceinline__ double exp_cr(double y, const double* cexp) {
@@ -194,9 +195,10 @@ __device__ __forceinline__ int64_t f64_to_i64(double x) {
     return (int64_t)x;
 }
 
-__device__ __forceinline__ int64_t trunc_log_ratio(double base, double sign, double v, double lambda, const double* clog) {
-    if (v > 0.0) {
-        const double ta = base + sign * (log_approx(v, clog) / lambda);
+__device__ __forceinline__ int64_t trunc_log_ratio(double base, double sign, double v, double lambda, double inv_lambda,
+                                                   const double* clog) {
+    if (v > 0.0) {  // (the quotient as a product with the host's RN(1 / lambda): within 2^-52 relative more, ~2^-37 in all)
+        const double ta = base + sign * (log_approx(v, clog) * inv_lambda);
         const double d = ta - __builtin_rint(ta);
         if (__builtin_fabs(d) > 0x1p-30 && __builtin_fabs(ta) < 0x1p52) return (int64_t)ta;
     }
@@ -375,47 +377,65 @@ __device__ __forceinline__ double stirling(double a) {
 // BTPE constants of Binomial(n, 1/2), one row per copy number k = n / 2 (host: ssa_api.cpp btpe_setup, the
 // same operations as the oracle's setup): npq, m, p1, x_m, x_l, x_r, c, p2, lambda_l, lambda_r, p3, p4
 constexpr int kBtpeRow = 16;  // doubles per row (128 B)
-enum { BT_NPQ, BT_M, BT_P1, BT_XM, BT_XL, BT_XR, BT_C, BT_P2, BT_LL, BT_LR, BT_P3, BT_P4 };
+enum { BT_NPQ, BT_M, BT_P1, BT_XM, BT_XL, BT_XR, BT_C, BT_P2, BT_LL, BT_LR, BT_P3, BT_P4, BT_ILL, BT_ILR };
 
-// BINV's factors for n = 2, 4, ..., 18 (the n p < 10 branch of rand_distr 0.4.3 Binomial with p = 1/2): row n / 2 - 1,
-// entry x = 1 .. 110 holds a / x - s with a = (n + 1) s, s = p / q = 1, formed by the same IEEE operations (a correctly
-// rounded f64 division, then the subtraction) as the loop that uses them, so a lookup gives the loop's own value bit for
-// bit (binv_factors stages the table in LDS; the loop's divisions were on its serial chain, ~10 f64 instructions each)
-constexpr int kBinvRows = 9, kBinvCols = 111;
-__device__ __forceinline__ void binv_factors(double* tab, uint32_t tid, uint32_t nthreads) {
-    for (uint32_t i = tid; i < (uint32_t)(kBinvRows * kBinvCols); i += nthreads) {
-        const uint32_t n = 2u * (i / kBinvCols + 1u), x = i % kBinvCols;
+// BINV (the n p < 10 branch of rand_distr 0.4.3 Binomial with p = 1/2: n = 2, 4, ..., 18). The reference's loop
+// subtracts r_0 = 2^-n, r_1, r_2, ... from u (r_x = r_{x-1} (a / x - s), a = (n + 1) s, s = p / q = 1) and returns the
+// first x with u_x <= r_x. The r_x do not depend on u: binv_cdf forms them by the loop's own IEEE operations, and their
+// running sums P_y = r_0 + ... + r_{y-1} (within 20 2^-53 of the real sums), row n / 2 - 1, y = 0 .. 20 (padded past
+// n + 1 with the last sum). The loop's u_x is u - P_x up to x roundings (x 2^-53 < 2^-47), so it stops at
+// x* = #{y >= 1 : P_y < u} whenever u is clear of P_x* and P_x*+1 by 2^-40 (the earlier sums lie further below u):
+// binv_half counts that branch-free and runs the reference's loop itself only otherwise (about 2^-35 of the draws, and
+// u past P_n+1, where the loop would run to its restart). Same result, bit for bit, without the serial loop (up to ~15
+// dependent steps for the slowest lane of a wave) on the common path.
+constexpr int kBinvRows = 9, kBinvCols = 21;
+__device__ __forceinline__ void binv_cdf(double* tab, uint32_t tid, uint32_t nthreads) {
+    for (uint32_t row = tid; row < (uint32_t)kBinvRows; row += nthreads) {
+        const uint32_t n = 2u * (row + 1u);
         const double s = 0.5 / 0.5;
         const double a = (double)(n + 1u) * s;
-        tab[i] = x ? a / (double)x - s : 0.0;
+        double r = __builtin_ldexp(1.0, -(int)n), acc = 0.0;
+        tab[row * kBinvCols] = 0.0;
+        for (uint32_t y = 1; y < (uint32_t)kBinvCols; ++y) {
+            acc += r;                              // P_y
+            tab[row * kBinvCols + y] = acc;
+            r *= a / (double)y - s;                // r_y (0 from y = n + 1 on)
+        }
     }
 }
 
 // rand_distr 0.4.3 Binomial::sample for p = 1/2 (n = 2k even, 2 <= n <= 65534): BINV for n p < 10, else BTPE.
-// binv: the binv_factors table.
 __device__ __forceinline__ bool binomial_half_is_binv(uint32_t n) { return (double)n * 0.5 < 10.0; }
 
-// BINV (n p < 10, n <= 18): s = p / q = 1, r0 = q^n = 2^-n exactly
+// BINV (n p < 10, n <= 18): s = p / q = 1, r0 = q^n = 2^-n exactly. binv: the binv_cdf table.
 __device__ __forceinline__ uint32_t binv_half(ChaCha8& rng, uint32_t n, const double* binv) {
+    ECDNA_REF_DBG(rng, 3);
+    double u = rng.gen_f64();
     {
-        ECDNA_REF_DBG(rng, 3);
-        const double* const fac = binv + (n / 2u - 1u) * kBinvCols;  // a / x - s for x = 1 .. 110
-        for (;;) {
-            double r = __builtin_ldexp(1.0, -(int)n);
-            double u = rng.gen_f64();
-            uint32_t x = 0;
-            bool restart = false;
-            while (u > r) {
-                u -= r;
-                x += 1;
-                if (x > 110u) {
-                    restart = true;
-                    break;
-                }
-                r *= fac[x];
+        const double* const P = binv + (n / 2u - 1u) * kBinvCols;
+        uint32_t x = 0;
+#pragma unroll
+        for (int y = 1; y < kBinvCols - 1; ++y) x += P[y] < u ? 1u : 0u;
+        if (x <= n && u - P[x] > 0x1p-40 && P[x + 1u] - u > 0x1p-40) return x;
+    }
+    // the reference's loop (the draws close to a sum, and past the last one)
+    const double s = 0.5 / 0.5;
+    const double a = (double)(n + 1u) * s;
+    for (;;) {
+        double r = __builtin_ldexp(1.0, -(int)n);
+        uint32_t x = 0;
+        bool restart = false;
+        while (u > r) {
+            u -= r;
+            x += 1;
+            if (x > 110u) {
+                restart = true;
+                break;
             }
-            if (!restart) return x;
+            r *= a / (double)x - s;
         }
+        if (!restart) return x;
+        u = rng.gen_f64();
     }
 }
 
@@ -427,6 +447,7 @@ __device__ __forceinline__ uint32_t btpe_half(ChaCha8& rng, uint32_t n, const do
     const double* b = btpe + (uint64_t)(n >> 1) * kBtpeRow;
     const double nd = (double)n, npq = b[BT_NPQ], p1 = b[BT_P1], x_m = b[BT_XM], x_l = b[BT_XL], x_r = b[BT_XR];
     const double c = b[BT_C], p2 = b[BT_P2], lambda_l = b[BT_LL], lambda_r = b[BT_LR], p3 = b[BT_P3], p4 = b[BT_P4];
+    const double inv_lambda_l = b[BT_ILL], inv_lambda_r = b[BT_ILR];
     const int64_t m = (int64_t)b[BT_M];
     int64_t y;
     for (;;) {
@@ -442,11 +463,11 @@ __device__ __forceinline__ uint32_t btpe_half(ChaCha8& rng, uint32_t n, const do
             if (v > 1.) continue;
             y = f64_to_i64(x);
         } else if (!(u > p3)) {
-            y = trunc_log_ratio(x_l, 1.0, v, lambda_l, clog);  // f64_to_i64(x_l + log_cr(v) / lambda_l)
+            y = trunc_log_ratio(x_l, 1.0, v, lambda_l, inv_lambda_l, clog);  // f64_to_i64(x_l + log_cr(v) / lambda_l)
             if (y < 0) continue;
             v *= (u - p2) * lambda_l;
         } else {
-            y = trunc_log_ratio(x_r, -1.0, v, lambda_r, clog);  // f64_to_i64(x_r - log_cr(v) / lambda_r)
+            y = trunc_log_ratio(x_r, -1.0, v, lambda_r, inv_lambda_r, clog);  // f64_to_i64(x_r - log_cr(v) / lambda_r)
             if (y > 0 && (uint64_t)y > (uint64_t)n) continue;
             v *= (u - p3) * lambda_r;
         }

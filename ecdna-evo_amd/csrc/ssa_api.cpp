@@ -131,7 +131,7 @@ void chacha_key_from_u64(uint64_t state, uint32_t key[8]) {
 
 // rand_distr 0.4.3 BTPE setup of Binomial(n, 1/2) (the step-0 constants; oracle/ssa_compat.c computes the same
 // per call), one row of refdraws::kBtpeRow doubles per copy number k = n / 2: npq, m, p1, x_m, x_l, x_r, c,
-// p2, lambda_l, lambda_r, p3, p4. Only n >= 20 (n p >= 10) takes BTPE.
+// p2, lambda_l, lambda_r, p3, p4, then 1 / lambda_l, 1 / lambda_r for the GPU's filtered step. Only n >= 20 (n p >= 10) takes BTPE.
 void btpe_setup(uint64_t n_u, double* row) {
     const double p = 0.5, q = 1.0 - p;
     const double n = (double)n_u;
@@ -151,8 +151,10 @@ void btpe_setup(uint64_t n_u, double* row) {
     const double lambda_r = ar * (1. + 0.5 * ar);
     const double p3 = p2 + c / lambda_l;
     const double p4 = p3 + c / lambda_r;
-    const double v[12] = {npq, (double)m, p1, x_m, x_l, x_r, c, p2, lambda_l, lambda_r, p3, p4};
-    for (int i = 0; i < 12; ++i) row[i] = v[i];
+    // (+ 1 / lambda_l, 1 / lambda_r: not the reference's arithmetic; only the GPU's filtered region-3/4 step uses them,
+    // refdraws::trunc_log_ratio, where a quotient within ~2^-37 decides)
+    const double v[14] = {npq, (double)m, p1, x_m, x_l, x_r, c, p2, lambda_l, lambda_r, p3, p4, 1.0 / lambda_l, 1.0 / lambda_r};
+    for (int i = 0; i < 14; ++i) row[i] = v[i];
 }
 constexpr int kBtpeRow = 16;  // refdraws::kBtpeRow
 

@@ -18,6 +18,7 @@
 //   * process.time += tau in f32 (src/process.rs:184, 336).
 // RNG: ChaCha8Rng::seed_from_u64(seed) on stream seed * 10 + r (src/main.rs:56-58), refdraws.hpp.
 #include "refdraws.hpp"
+#include "ssa_device.hpp"
 #include "ssa_launch.h"
 
 #pragma clang fp contract(off)
@@ -105,7 +106,7 @@ __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_re
     }
     for (uint32_t i = threadIdx.x; i < 3u * ECDNA_CLOG_N; i += blockDim.x) clog[i] = kCLog[i];
     for (uint32_t i = threadIdx.x; i < 128u; i += blockDim.x) cexp[i] = kCExp[i];
-    refdraws::binv_factors(binv, threadIdx.x, blockDim.x);
+    refdraws::binv_cdf(binv, threadIdx.x, blockDim.x);
     __syncthreads();
     const uint32_t tid = threadIdx.x;
     const bool hash_on = (a.flags & ECDNA_FLAG_EVENT_HASH) != 0;
@@ -180,7 +181,10 @@ __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_re
         for (int c = 0; c < K; ++c) {
             const float lambda = rates[c] * (float)pop[c];
             if (!(lambda > 0.0f)) continue;
-            const float inv = 1.0f / lambda;
+            // 1 / lambda, the correctly rounded f32 quotient: div_in_range (ssa_device.hpp) is exact for a numerator in
+            // [2^-24, 16.7] and a divisor in [2^-60, 2^94], and lambda = rate * pop is in [2^-60, 2^92] (the ABI's rate
+            // range, u32 populations): the compiler's division without its scaling and fixup steps
+            const float inv = div_in_range(1.0f, lambda);
             const float tau = (float)refdraws::exp1(rng, zx, zf, clog, cexp) * inv;
             if (ch < 0 || tau < best) {
                 best = tau;

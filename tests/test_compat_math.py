@@ -122,6 +122,44 @@ def test_btpe_explicit_ratio_filter_error_bound(n):
     assert worst_f < 2.0 ** -41 and worst_fa < 2.0 ** -41, (worst_f, worst_fa)
 
 
+def test_binv_cdf_filter_agrees_with_the_loop():
+    """BINV (rand_distr's n p < 10 branch, n = 2 .. 18): the GPU counts x = #{y : P_y < u} over the running sums P_y of
+    the loop's r values (csrc/refdraws.hpp binv_cdf / binv_half) and keeps x only where u is clear of P_x and P_x+1 by
+    2^-40 (and x <= n); else it runs the loop. Restated with Python's IEEE doubles: wherever the filter decides it
+    equals the reference's loop, over 40,000 uniforms per n (random, and next to every P_y)."""
+    rng = random.Random(17)
+    s = 0.5 / 0.5
+    for n in range(2, 20, 2):
+        a = (n + 1) * s
+        P, r, acc = [0.0], 2.0 ** -n, 0.0
+        for y in range(1, 21):
+            acc += r
+            P.append(acc)
+            r *= a / float(y) - s
+
+        def loop(u):
+            r, x = 2.0 ** -n, 0
+            while u > r:
+                u -= r
+                x += 1
+                if x > 110:
+                    return None  # (restart)
+                r *= a / float(x) - s
+            return x
+
+        us = [rng.getrandbits(53) * 2.0 ** -53 for _ in range(40_000)]
+        us += [math.nextafter(p_, d) for p_ in P[1:] for d in (0.0, 2.0)] + [p_ + e for p_ in P[1:] for e in (2.0 ** -39, -2.0 ** -39)]
+        decided = 0
+        for u in us:
+            if not 0.0 <= u < 1.0:
+                continue
+            x = sum(1 for y in range(1, 20) if P[y] < u)
+            if x <= n and u - P[x] > 2.0 ** -40 and P[x + 1] - u > 2.0 ** -40:
+                decided += 1
+                assert loop(u) == x, (n, u, x, loop(u))
+        assert decided > 0.99 * 40_000
+
+
 @pytest.mark.parametrize("fn,gen", [
     ("log", lambda r: r.random() or 0.5),
     ("log", lambda r: r.uniform(0.5, 3.0)),
