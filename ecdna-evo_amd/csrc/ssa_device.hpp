@@ -84,31 +84,40 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, const PhiloxKeys& rk) {
     return c;
 }
 
-// The bin store's event block is Philox((e, 0, rid_lo, rid_hi)): round 0's c.z product and the words
-// it is XORed with depend only on the replicate, so they are formed once per replicate.
+// The bin store's event block is Philox((e, 0, rid_lo, rid_hi)): round 0's c.z product and the words it is XORed with
+// depend only on the replicate, and so do round 1's c.x product (c.x = round 0's output 0) and the key words XORed into
+// round 1's outputs 0 and 2. They are formed once per replicate; an event's round 1 is then one product and three
+// two-input XORs (the e-dependent part), against two products and two three-input XORs. Same function.
 struct PhiloxEventPre {
-    uint32_t x0, x1, x2;  // round-0 outputs 0 and 1; rid_hi ^ k1[0] for output 2
+    uint32_t x1k;  // round-0 output 1 ^ k0[1]
+    uint32_t x2;   // rid_hi ^ k1[0] (round-0 output 2 is hi(M0 e) ^ x2)
+    uint32_t y2k;  // hi(M0 * round-0 output 0) ^ k1[1]
+    uint32_t y3;   // lo(M0 * round-0 output 0): round-1 output 3
 };
 
 __device__ __forceinline__ PhiloxEventPre philox_event_pre(uint32_t rid_lo, uint32_t rid_hi, const PhiloxKeys& rk) {
     const uint64_t p1 = (uint64_t)kPhiloxM1 * rid_lo;
+    const uint32_t x0 = (uint32_t)(p1 >> 32) ^ rk.k0[0];  // round-0 output 0 (c.y = 0)
+    const uint64_t q0 = (uint64_t)kPhiloxM0 * x0;          // round 1's c.x product
     PhiloxEventPre p;
-    p.x0 = (uint32_t)(p1 >> 32) ^ rk.k0[0];  // (c.y = 0)
-    p.x1 = (uint32_t)p1;
+    p.x1k = (uint32_t)p1 ^ rk.k0[1];
     p.x2 = rid_hi ^ rk.k1[0];
+    p.y2k = (uint32_t)(q0 >> 32) ^ rk.k1[1];
+    p.y3 = (uint32_t)q0;
     return p;
 }
 
 // == philox4x32_10(make_uint4(e, 0, rid_lo, rid_hi), rk) for the pre formed from (rid_lo, rid_hi)
 template <bool B3 = false>
 __device__ __forceinline__ uint4 philox_event(uint32_t e, const PhiloxEventPre& pre, const PhiloxKeys& rk) {
-    const uint64_t p0 = (uint64_t)kPhiloxM0 * e;
-    uint4 c = make_uint4(pre.x0, pre.x1, (uint32_t)(p0 >> 32) ^ pre.x2, (uint32_t)p0);
+    const uint64_t p0 = (uint64_t)kPhiloxM0 * e;                        // round 0's c.x product
+    const uint64_t q1 = (uint64_t)kPhiloxM1 * ((uint32_t)(p0 >> 32) ^ pre.x2);  // round 1's c.z product
+    uint4 c = make_uint4((uint32_t)(q1 >> 32) ^ pre.x1k, (uint32_t)q1, pre.y2k ^ (uint32_t)p0, pre.y3);
 #pragma unroll
-    for (int r = 1; r < 10; ++r) {
+    for (int r = 2; r < 10; ++r) {
         const uint64_t q0 = (uint64_t)kPhiloxM0 * c.x;
-        const uint64_t q1 = (uint64_t)kPhiloxM1 * c.z;
-        c = make_uint4(xor3<B3>((uint32_t)(q1 >> 32), c.y, rk.k0[r]), (uint32_t)q1,
+        const uint64_t q1r = (uint64_t)kPhiloxM1 * c.z;
+        c = make_uint4(xor3<B3>((uint32_t)(q1r >> 32), c.y, rk.k0[r]), (uint32_t)q1r,
                        xor3<B3>((uint32_t)(q0 >> 32), c.w, rk.k1[r]), (uint32_t)q0);
     }
     return c;

@@ -456,9 +456,9 @@ constexpr int kCpolSc1 = 16;  // buffer cache policy: sc1 (gfx940+ bit 4)
 #ifndef ECDNA_FF_STAY8
 #define ECDNA_FF_STAY8 7   // keep going while >= this many eighths of the entered lanes do
 #endif
-// the entry test is a mask of the wave-uniform iteration counter (ff_tick & (N - 1)): N must be a power of two
-static_assert(ECDNA_FF_TEST_EVERY > 0 && (ECDNA_FF_TEST_EVERY & (ECDNA_FF_TEST_EVERY - 1)) == 0,
-              "ECDNA_FF_TEST_EVERY must be a power of two");
+// the entry test runs when a wave-uniform countdown reaches 0 (reset to ECDNA_FF_TEST_EVERY, or to 1 while the wave
+// fast-forwards)
+static_assert(ECDNA_FF_TEST_EVERY > 0, "ECDNA_FF_TEST_EVERY must be positive");
 constexpr uint32_t kFfMax = ECDNA_FF_MAX;  // N- fast-forward: events per full iteration at most
 
 #ifdef ECDNA_ILP_BUILD
@@ -651,7 +651,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
     // the Philox blocks' XOR3 as the compiler builtin (ssa_device.hpp xor3) in the K = 64 / 256 and paired instances
     // (C4, C5 shards: waves that drain or run alone); the issue-bound K = 32 kernel (C3) keeps the asm form
     constexpr bool kB3 = NG >= 8 || PAIR;
-    PhiloxEventPre pre{0u, 0u, 0u};  // the replicate-only part of round 0
+    PhiloxEventPre pre{0u, 0u, 0u, 0u};  // the replicate-only part of rounds 0 and 1
     PATH_STATS_DECL;
     const uint32_t stop32 = a.stop_cells < 0xffffffffull ? (uint32_t)a.stop_cells : 0xffffffffu;
     // PAIR: a helper serves lane - 32 and never owns a replicate
@@ -851,7 +851,9 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
     const uint32_t tick_mask = rot ? ((1u << a.rot_tick_log2) - 1u) : 0xffffffffu;
     uint32_t it = 0;
     bool pinned = false;
-    uint32_t ff_tick = 0;  // N- fast-forward: iterations (wave-uniform) and the wave's mode
+    // N- fast-forward: the entry test's countdown (wave-uniform: three scalar instructions per iteration, where a mask of
+    // an iteration counter or-ed with the mode took eight) and the wave's mode
+    uint32_t ff_cd = ECDNA_FF_TEST_EVERY;
     bool ff_mode = false;
 
 #ifdef ECDNA_ROT_STATS
@@ -866,7 +868,6 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
     for (;;) {
         CYC_MARK(2);
         CYC_ADD(3, 1);
-        ++ff_tick;
         if (rot && ((++it & tick_mask) == 0u)) {  // ---- rotation tick (wave-uniform)
 #ifdef ECDNA_ROT_STATS
             const unsigned long long c0 = clock64();
@@ -1059,11 +1060,10 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                 nsp = 0;
                 h = kFnvOffset;
                 sj = 0;
-                if (ns + nb == 0 && nm == 0) {  // ensure!(!distribution.is_empty()) src/process.rs:88, 232
-                    err = ECDNA_REP_ERR_EMPTY;
-                    stop = ECDNA_STOP_ERROR;
-                    active = false;
-                }
+                // ensure!(!distribution.is_empty()) src/process.rs:88, 232: the error is recorded here and the replicate
+                // stops at this iteration's stop test (a0 = 0 there; the reason follows err), so that every lane that
+                // reaches the event path without PAIR holds a replicate and the path needs no skip branch
+                if (ns + nb == 0 && nm == 0) err = ECDNA_REP_ERR_EMPTY;
             }
             }  // (a replicate claimed)
         }
@@ -1080,7 +1080,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
         // condition, untouched: the full event below draws that same event. Snapshots (checked per
         // event) keep the full loop. The entry test runs every 32nd iteration (ECDNA_FF_TEST_EVERY) while the wave is not
         // fast-forwarding, every iteration while it is (wave-uniform control: ballots at the loop top).
-        if (BD && kFfMax && !n_snap && (ff_mode || (ff_tick & (ECDNA_FF_TEST_EVERY - 1u)) == 0u)) {
+        if (BD && kFfMax && !n_snap && --ff_cd == 0u) {
             const uint32_t npf = ns + nb;  // n+ is fixed during N- events
             const float fpf = (float)npf;
             const double pbf = (double)(rb1 * fpf), pdf = (double)(rd1 * fpf);
@@ -1088,20 +1088,22 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
             const bool heavy = active && pm * 8.0f >= (pm + (float)pbf + (float)pdf) * (float)ECDNA_FF_ENTER8;  // (speed only)
             const uint32_t n_in = (uint32_t)__builtin_popcountll(__ballot(active));
             ff_mode = n_in != 0u && (uint32_t)__builtin_popcountll(__ballot(heavy)) * 8u >= n_in * ECDNA_FF_ENTER8;
+            ff_cd = ff_mode ? 1u : ECDNA_FF_TEST_EVERY;
             CYC_ADD(4, ff_mode ? 1u : 0u);
             if (PAIR && ff_mode) {
                 // Paired steps (DESIGN.md §5 "Paired lanes"): every lane forms one Philox block and soft log with
                 // the same instructions, the owner (lane l) for its event e, the helper (lane l + 32) for the
-                // owner's e + 1 from the owner's replicate-only round-0 words; the owner pulls the helper's words
-                // (v_permlane32_swap) and runs the state-dependent part of e, then of e + 1. Same draws, same
+                // owner's e + 1 from the owner's replicate-only round-0 and round-1 words; the owner pulls the helper's
+                // words (v_permlane32_swap) and runs the state-dependent part of e, then of e + 1. Same draws, same
                 // arithmetic, same order as the unpaired loop below: results are identical.
                 bool go = active;
                 PhiloxEventPre hp = pre;
                 {
-                    const auto x0 = __builtin_amdgcn_permlane32_swap(pre.x0, pre.x0, false, false);
-                    const auto x1 = __builtin_amdgcn_permlane32_swap(pre.x1, pre.x1, false, false);
+                    const auto x1k = __builtin_amdgcn_permlane32_swap(pre.x1k, pre.x1k, false, false);
                     const auto x2 = __builtin_amdgcn_permlane32_swap(pre.x2, pre.x2, false, false);
-                    if (helper) hp = PhiloxEventPre{x0[0], x1[0], x2[0]};  // (lanes >= 32 receive lanes < 32)
+                    const auto y2k = __builtin_amdgcn_permlane32_swap(pre.y2k, pre.y2k, false, false);
+                    const auto y3 = __builtin_amdgcn_permlane32_swap(pre.y3, pre.y3, false, false);
+                    if (helper) hp = PhiloxEventPre{x1k[0], x2[0], y2k[0], y3[0]};  // (lanes >= 32 receive lanes < 32)
                 }
                 // One paired step: events e and e + 1 of the owner, branch-free. Both events' propensities,
                 // stop tests and channels are formed from the state as it would be after e (e + 1 reads n-
@@ -1112,7 +1114,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                 // blocks and soft-log table loads are issued ahead, while this step's events run (used only if
                 // both events commit; otherwise the lane has left). A lone wave pays roughly its instruction
                 // count here (forming e + 1 for both possible n- alongside e, to cut the chain, was slower).
-                // (one Philox instruction stream for both halves: the counter and the round-0 words are selected
+                // (one Philox instruction stream for both halves: the counter and the replicate words are selected
                 // per lane; two philox_event calls under a per-lane select would run both streams on every lane)
                 // ctr: the lane's event counter, e for an owner and its owner's e + 1 for a helper; a step that
                 // continues advances both by 2 (a lane that commits fewer leaves, and its next words go unused)
@@ -1245,30 +1247,37 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
         }
         CYC_MARK(1);
         CYC_ADD(6, __builtin_popcountll(__ballot(active)));
-        if (!active) continue;  // (an empty initial distribution)
+        if (PAIR && !active) continue;  // (a helper, or an owner with nothing left)
         PATH_STAT(0);
         PATH_STAT_LANES(1);
         const uint32_t np = ns + nb;
 
         // propensities rate_i * population_i over [n-, n+(, n-, n+)] in f32 (the reference's own, src/main.rs:67, 139),
         // their cumulative sums in f64 (draw mapping v7); the time step divides by a0 = RN32(A)
-        const float fm = (float)nm, fp = (float)np;
-        const double cA = (double)(rb0 * fm);
-        const double cB = cA + (double)(rb1 * fp);
+        // (the four f32 products as two v_pk_mul_f32 of the rate pairs (b-, b+) and (d-, d+) by (n-, n+): the same
+        // IEEE products)
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        const f32x2 pops = {(float)nm, (float)np};
+        const f32x2 rbv = {rb0, rb1}, rdv = {rd0, rd1};
+        const f32x2 pb = rbv * pops;
+        const double cA = (double)pb.x;
+        const double cB = cA + (double)pb.y;
         double cC = cB, A = cB;
         if (BD) {
-            cC = cB + (double)(rd0 * fm);
-            A = cC + (double)(rd1 * fp);
+            const f32x2 pd = rdv * pops;
+            cC = cB + (double)pd.x;
+            A = cC + (double)pd.y;
         }
         const float a0 = (float)A;
         // stop checks: one test here, the reason only when a lane stops
         const bool t_over = f32t ? (t32 >= a.max_time32) : (t >= a.max_time);
         const bool cells_over = nm + np >= stop32;  // (u32: cell counts stay below 2^32)
         if ((e >= a.max_iter) || cells_over || t_over || !(a0 > 0.0f)) {
-            stop = (e >= a.max_iter) ? (uint32_t)ECDNA_STOP_MAX_ITER
-                   : cells_over     ? (uint32_t)ECDNA_STOP_MAX_CELLS
-                   : t_over         ? (uint32_t)ECDNA_STOP_MAX_TIME
-                                    : (uint32_t)ECDNA_STOP_ABSORBING;
+            stop = err                 ? (uint32_t)ECDNA_STOP_ERROR  // (an empty initial distribution: ERR_EMPTY)
+                   : (e >= a.max_iter) ? (uint32_t)ECDNA_STOP_MAX_ITER
+                   : cells_over        ? (uint32_t)ECDNA_STOP_MAX_CELLS
+                   : t_over            ? (uint32_t)ECDNA_STOP_MAX_TIME
+                                       : (uint32_t)ECDNA_STOP_ABSORBING;
             active = false;
         } else {
             if (n_snap) {  // src/process.rs:122-145, as in ssa_stepper
@@ -1335,6 +1344,10 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
             // 29.3 -> 28.8 s; with u16 counters, the C4 shard, whose waves share their SIMD until the drain, lost
             // 5 %: profiles/r04p_large_pick_ahead_ab.txt)
             constexpr bool kAhead = SCH == 1 && NG == 8 && C32;
+            // the largest n = 2k whose segregation the event's own words cover: w3 (32 bits) and, when there is one, the
+            // first spare (64); 0 once a Lemire rejection has consumed stream words (the general path then reads on
+            // from the stream position). One compare against it replaces the position and range tests.
+            uint32_t seg_lim = 32u << min(nsp, 1u);
             uint32_t k_ahead = 0, tail_ahead = 0;
             bool ahead = false;
             if (SCH == 1) {
@@ -1355,12 +1368,13 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                         }
                     }
                 }
-                k = bin_find(small ? idx : 0u);
+                k = bin_find(idx);  // (any index reads the same in-range counters; k of a large pick is replaced below)
                 if (nplus_ev & (((uint32_t)m < np) | !small)) {  // Lemire rejection or the large-k row (rare)
                     if ((uint32_t)m < np) {
                         PATH_STAT(3);
                         const uint32_t thr = (0u - np) % np;
                         while ((uint32_t)m < thr) m = (uint64_t)ws.next() * np;
+                        if (ws.pos != 1u) seg_lim = 0u;
                         idx = (uint32_t)(m >> 32);
                         small = idx < ns;
                         if (small) k = bin_find(idx);
@@ -1375,10 +1389,11 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     PATH_STAT(3);
                     const uint32_t thr = (0u - np) % np;
                     while ((uint32_t)m < thr) m = (uint64_t)ws.next() * np;
+                    if (ws.pos != 1u) seg_lim = 0u;
                 }
                 idx = (uint32_t)(m >> 32);
                 small = idx < ns;
-                k = bin_find(small ? idx : 0u);
+                k = bin_find(idx);
                 if (nplus_ev && !small) {  // large-k row (rare)
                     PATH_STAT(4);
                     k = gload_u16_l2(row + (idx - ns));
@@ -1393,17 +1408,17 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
             uint32_t ev_err = 0;
             if (SEG != ECDNA_SEG_DETERMINISTIC) {
                 // popcount of the stream's next n bits: w3 alone (k <= 16) or w3 and the first spare (k <= 32)
-                const bool fast1 = ws.pos == 1 && n <= 32u;
-                const bool fast2 = ws.pos == 1 && n > 32u && n <= 64u && nsp >= 1u;
-                const bool fast = fast1 || fast2;
+                const bool fast = n <= seg_lim;
                 // branch-free: the low n bits of the 64-bit word (spare0 : w3), moved to its top by one shift (the
                 // value only counts where fast: 1 <= n <= 64)
                 const uint64_t x64 = (((uint64_t)sp0 << 32) | w.w) << ((64u - n) & 63u);
                 k1v = __popc((uint32_t)(x64 >> 32)) + __popc((uint32_t)x64);
-                if (prolif && fast) ws.pos = fast1 ? 2u : 3u;
-                if (prolif && !fast && k <= 32767u) {  // larger copy numbers or a rejected pick: more words
-                    PATH_STAT(5);
-                    k1v = ws.binomial_half<kAhead, kB3>(n, rk);
+                if (prolif && fast) ws.pos = (n + 63u) >> 5;  // 2 (w3 used) or 3 (w3 and the first spare)
+                if (prolif && !fast) {  // larger copy numbers or a rejected pick: more words
+                    if (k <= 32767u) {  // (larger ones stop with ECDNA_REP_ERR_OVERFLOW below)
+                        PATH_STAT(5);
+                        k1v = ws.binomial_half<kAhead, kB3>(n, rk);
+                    }
                 }
                 if (SEG == ECDNA_SEG_BINOMIAL_NO_UNEVEN && prolif && (k1v == 0u || k1v == n)) {
                     // src/segregation.rs:157-174: redraw while uneven (the first draw above was try 1)
@@ -1427,8 +1442,6 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     un = (k1v == 0u || k1v == n) ? (SEG == ECDNA_SEG_BINOMIAL_NO_NMINUS ? 2u : 1u) : 0u;
             }
             CYC_MARK(11);
-            // checked_mul panic (src/proliferation.rs:63-67)
-            ev_err = (k > 32767u) ? (uint32_t)ECDNA_REP_ERR_OVERFLOW : ev_err;
             // the indexing invariant (ECDNA_REP_ERR_INTERNAL, ABI v11), in the runtime-flags instances (TF = 1; the
             // bench's TF = 0 instances keep their event path): an N+ event needs an N+ cell and a pick below n+
             // (np == 0 gives idx 0). Unreachable under draw mapping v7; a broken channel would otherwise swap_remove
@@ -1437,39 +1450,36 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
             // daughters (none for a death): [k1, k2] on an even split, [n] on an uneven one
             const uint32_t da = (un == 0u) ? k1v : n;
             const uint32_t db = n - k1v;
-            const bool has_a = prolif, has_b = prolif && un == 0u;
-            const bool sa = has_a && da <= K, sb = has_b && db <= K;
-            // capacity checks: the N+ row (cell_cap) and the large-k row (big_cap <= cell_cap). After an
-            // event the large-k row holds at most np + 1 cells, so neither can overflow while
-            // np + 1 <= big_cap: one compare on the event path, the checks themselves in a rare block
-            // (C3: 88.0 ms per launch without any big_cap check, 91.8 with it on every event, 89.3 gated).
-            if (np + 1u > big_cap_v) {
-                PATH_STAT(7);
-                KArgs* const ra = rare_args();
-                if (prolif && ev_err == 0u && un == 0u && np + 1u > ra->cell_cap) ev_err = ECDNA_REP_ERR_CELL_CAP;
-                const uint32_t nb_new = nb - (small ? 0u : 1u) + ((has_a && !sa) ? 1u : 0u) + ((has_b && !sb) ? 1u : 0u);
-                if (prolif && ev_err == 0u && ((has_a && !sa) || (has_b && !sb)) && nb_new > ra->big_cap)
-                    ev_err = ECDNA_REP_ERR_CELL_CAP;
-            }
-            CYC_MARK(12);
-            if ((prolif && ev_err) || internal) {  // the event is not applied; the replicate stops (rare)
-                err = internal ? (uint32_t)ECDNA_REP_ERR_INTERNAL : ev_err;
-                stop = ECDNA_STOP_ERROR;
-                active = false;
-            } else {
-                const float tau = div_in_range(softlog_neg(w.x, logtab), a0);
-                CYC_MARK(13);
-
-                const uint32_t ns_old = ns;
-                // common case: every copy number involved is binned -> LDS only, no branch
-                // (bin_add_ev clamps its copy number into range, so lanes adding 0 need no select)
-                bin_add_ev(k, (nplus_ev && small) ? 0xffffffffu : 0u);
-                bin_add_ev(da, sa ? 1u : 0u);
-                bin_add_ev(db, sb ? 1u : 0u);
-                ns = ns - ((nplus_ev && small) ? 1u : 0u) + (sa ? 1u : 0u) + (sb ? 1u : 0u);
-                if (nplus_ev && (!small || (has_a && !sa) || (has_b && !sb))) {  // the large-k row (rare)
+            const bool has_a = prolif, has_b = prolif & (un == 0u);
+            const bool sa = has_a & (da <= K), sb = has_b & (db <= K);
+            // the large-k row takes part (bitwise: no short-circuit control flow on the common path)
+            const bool row_ev = nplus_ev & (!small | (has_a & !sa) | (has_b & !sb));
+            // The event's rare work in one branch: the error checks, the capacity checks and the large-k row's update;
+            // the common path carries that branch and the commit's (apply), where it carried three (the capacity gate,
+            // the error if / else, the row update inside the commit). capacity: the N+ row (cell_cap) and the large-k
+            // row (big_cap <= cell_cap); after an event the large-k row holds at most np + 1 cells, so neither can
+            // overflow while np + 1 <= big_cap (C3: 88.0 ms per launch without any big_cap check, 91.8 with it on every
+            // event, 89.3 gated). checked_mul: a copy number above 32767 is a large picked cell, which row_ev covers.
+            bool apply = true;
+            if (row_ev | (np + 1u > big_cap_v) | (prolif & (ev_err != 0u)) | internal) {
+                if (k > 32767u) ev_err = ECDNA_REP_ERR_OVERFLOW;  // checked_mul panic (src/proliferation.rs:63-67)
+                if (np + 1u > big_cap_v) {
+                    PATH_STAT(7);
+                    KArgs* const ra = rare_args();
+                    if (prolif && ev_err == 0u && un == 0u && np + 1u > ra->cell_cap) ev_err = ECDNA_REP_ERR_CELL_CAP;
+                    const uint32_t nb_new =
+                        nb - (small ? 0u : 1u) + ((has_a && !sa) ? 1u : 0u) + ((has_b && !sb) ? 1u : 0u);
+                    if (prolif && ev_err == 0u && ((has_a && !sa) || (has_b && !sb)) && nb_new > ra->big_cap)
+                        ev_err = ECDNA_REP_ERR_CELL_CAP;
+                }
+                apply = !((prolif && ev_err) || internal);
+                if (!apply) {  // the event is not applied; the replicate stops
+                    err = internal ? (uint32_t)ECDNA_REP_ERR_INTERNAL : ev_err;
+                    stop = ECDNA_STOP_ERROR;
+                    active = false;
+                } else if (row_ev) {  // the large-k row (ns is the event's; the bins are updated below)
                     PATH_STAT(6);
-                    uint32_t open = small ? 0xffffffffu : idx - ns_old;  // B slot freed by a large picked cell
+                    uint32_t open = small ? 0xffffffffu : idx - ns;  // B slot freed by a large picked cell
                     if (has_a && !sa) {
                         if (open != 0xffffffffu) {
                             row[open] = (uint16_t)da;
@@ -1492,6 +1502,17 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                         nb -= 1;
                     }
                 }
+            }
+            CYC_MARK(12);
+            if (apply) {
+                const float tau = div_in_range(softlog_neg(w.x, logtab), a0);
+                CYC_MARK(13);
+                // common case: every copy number involved is binned -> LDS only, no branch
+                // (bin_add_ev clamps its copy number into range, so lanes adding 0 need no select)
+                bin_add_ev(k, (nplus_ev && small) ? 0xffffffffu : 0u);
+                bin_add_ev(da, sa ? 1u : 0u);
+                bin_add_ev(db, sb ? 1u : 0u);
+                ns = ns - ((nplus_ev && small) ? 1u : 0u) + (sa ? 1u : 0u) + (sb ? 1u : 0u);
                 CYC_MARK(14);
                 spares_update(nplus_ev ? ws.pos : 0u, w.z, w.w, sp0, sp1, nsp);
                 nm = nm + ((!gA || (prolif && un == 1u)) ? 1u : 0u) - (death_nm ? 1u : 0u);

@@ -4,6 +4,8 @@
 #     suite      the full -m gpu suite on the working tree's library
 #     parity     the parity subset only (parity, random parity, rotation, drain, rare channels)
 #     ab_c3      C3 (K = 32) with each prebuilt library of LIBS, interleaved twice (tools/ab_libs.sh)
+#     stall      two PMC passes per library of LIBS: the SQ wave-cycle split, LDS / branch / fetch counters
+#     rcp        the time step's reciprocal against RN32(1 / b) for every f32 b the stepper divides by (tools/rcp_check)
 #     latency    C2, C4 rank-0 shard, C5 rank-0 shard with each library (tools/ab_latency.sh)
 #     pmc        one SQ-counter pass (VALU / SALU / LDS per wave-event of one C3 step) per library
 #     c3s        the C3 fixed-total shards (G = 1, 2, 4, 8; all ranks) with the working tree (tools/c3_strong.py)
@@ -60,6 +62,22 @@ for step in ${STEPS//,/ }; do
           SQ_WAVES SQ_BUSY_CYCLES -T --output-format csv -d gpurun_out/${TAG}_pmc_$n -o pmc -- python3 bench.py --steps 1 \
           --warmup 0 --no-cpu-baseline > gpurun_out/${TAG}_pmc_$n.log 2>&1
         python3 tools/ab_pmc_summary.py gpurun_out/${TAG}_pmc_$n gpurun_out/${TAG}_pmc_$n.log "$n" | tee -a gpurun_out/${TAG}_pmc.txt
+      done ;;
+    rcp)
+      rc=0; timeout -k 10 120 tools/rcp_check > gpurun_out/${TAG}_rcp_check.json || rc=$?
+      cat gpurun_out/${TAG}_rcp_check.json; [ $rc -le 1 ] || exit 1 ;;  # (1: mismatches found, reported)
+    stall)  # the SQ wave-cycle split (waiting on waitcnt / issue-stalled / issuing) and the LDS, branch and fetch counters
+      for n in $LIBS; do
+        k=0
+        for pass in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS" \
+                    "SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_IFETCH SQ_ACTIVE_INST_MISC SQ_BUSY_CYCLES SQ_INSTS_SMEM SQ_WAVES"; do
+          k=$((k + 1))
+          ECDNA_SSA_LIB=$L/$n/libecdna_ssa.so timeout -s KILL 300 rocprofv3 --pmc $pass -T --output-format csv \
+            -d gpurun_out/${TAG}_stall_${n}_$k -o pmc -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline \
+            > gpurun_out/${TAG}_stall_${n}_$k.log 2>&1
+          python3 tools/ab_pmc_summary.py gpurun_out/${TAG}_stall_${n}_$k gpurun_out/${TAG}_stall_${n}_$k.log "$n" all \
+            | tee -a gpurun_out/${TAG}_stall.txt
+        done
       done ;;
     c3s)
       timeout -k 10 300 python3 -u tools/c3_strong.py > gpurun_out/${TAG}_c3_strong.jsonl 2> gpurun_out/${TAG}_c3_strong.err
