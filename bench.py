@@ -526,10 +526,10 @@ def main():
             "scaling": "weak" if weak else "strong",
             "vs_baseline": None,
             # integer cell/counter work plus the reference's f32 propensities (src/main.rs:67, 139) and f32 time step;
-            # the channel's cumulative sums and the engine's clock in f64 (draw mapping v7)
+            # the channel's cumulative sums and the engine's clock in f64 (draw mapping v8)
             "dtype": "u16+f32" if refdraws else "u16+f32 (f64 channel sums and clock)",
             "draws": "reference (ChaCha8 seed*10+i, first-reaction, BINV/BTPE, f32 time; seed for seed)"
-                     if refdraws else "philox (the engine's draw mapping v7, DESIGN.md §3)",
+                     if refdraws else "philox (the engine's draw mapping v8, DESIGN.md §3)",
             "store": args.store,
             "data": "synthetic",
             "config": {

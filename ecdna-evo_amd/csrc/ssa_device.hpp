@@ -171,20 +171,19 @@ __device__ __forceinline__ float softlog_neg(uint32_t w, const float2* tab) { re
 // against the oracle's channel function, tests/native/device_math_check.cpp.)
 __host__ __device__ __forceinline__ double chan_target(uint32_t w, double a) { return ((double)w + 0.5) * a * 0x1p-32; }
 
-// n / d, the correctly rounded IEEE f32 quotient (the oracle's C division), for operands in the stepper's range.
-// LLVM lowers an f32 divide to v_div_scale x2, v_rcp_f32, the Newton step, the quotient and two residual
-// corrections, v_div_fmas and v_div_fixup; the scales, the scale flag of v_div_fmas and the fixup only act when an
-// operand, the quotient or a residual is near the denormal or overflow range, or on zero / inf / NaN divisors. The
-// time step divides a soft log in [2^-24, 16.7] by a total propensity in [2^-60, 2^94] (every rate 0 or in
-// [2^-60, 2^60], which ecdna_ssa_ctx_create requires; u32 populations; a0 > 0), so every intermediate is a normal
-// f32 and the same rcp / fma sequence without them yields the same bits.
-__device__ __forceinline__ float div_in_range(float n, float d) {
-    const float r0 = __builtin_amdgcn_rcpf(d);
-    const float r1 = fmaf(fmaf(-d, r0, 1.0f), r0, r0);
-    const float q0 = n * r1;
-    const float q1 = fmaf(fmaf(-d, q0, n), r1, q0);
-    return fmaf(fmaf(-d, q1, n), r1, q1);
-}
+// RN32(1 / d) from the hardware reciprocal and one Newton step: y = fma(fma(-d, r, 1), r, r), r = v_rcp_f32(d). For
+// every f32 d of the stepper's divisors (total propensities in [2^-60, 2^94]: every rate 0 or in [2^-60, 2^60], which
+// ecdna_ssa_ctx_create requires, u32 populations; reference-draws rates, the same range) y is the correctly rounded
+// reciprocal: checked on the GPU for all 1.3e9 f32 values in [2^-60, 2^95) (tools/rcp_check.hip, tests/test_gpu_rcp.py:
+// no mismatch). On the CPU (tests/native/device_math_check.cpp) the step from either faithful r (RD or RU of 1 / d)
+// gives RN(1 / d) for every d of a binade but one mantissa, 0x7fffff from RD (1 / d within 2^-49 of a midpoint), where
+// the hardware's r is RU. Draw mapping v8: the time step is RN32(softlog * RN32(1 / a0)), a product with
+// the correctly rounded reciprocal (v7 divided: the correctly rounded quotient took two more residual corrections, four
+// more instructions per event; the product differs from the quotient by at most one ulp). rcp_newton is the step from
+// a given r (host-callable: the CPU check feeds it RD and RU).
+__host__ __device__ __forceinline__ float rcp_newton(float d, float r) { return fmaf(fmaf(-d, r, 1.0f), r, r); }
+
+__device__ __forceinline__ float rcp_rn(float d) { return rcp_newton(d, __builtin_amdgcn_rcpf(d)); }
 
 // x << (s & 31) as one v_lshlrev_b32, which reads only the low five bits of its amount (C++ leaves a shift by
 // 32 or more undefined, so the compiler would keep an explicit mask)
@@ -369,10 +368,10 @@ struct WordStream {
 // single spare sent 3.5x more events to a second Philox block, a net loss at C3).
 __device__ __forceinline__ void spares_update(uint32_t used, uint32_t w2, uint32_t w3, uint32_t& s0, uint32_t& s1,
                                               uint32_t& nsp) {
-    const bool u0 = used == 0u, u1 = used == 1u, pop = used >= 3u;
+    const bool u0 = used == 0u, le1 = used <= 1u, pop = used >= 3u;  // (three compares: u1 = le1 & !u0)
     const uint32_t n1 = s1, n0 = s0;
-    s1 = u0 ? w2 : (u1 ? n0 : n1);
-    s0 = (used <= 1u) ? w3 : (pop ? n1 : n0);
+    s1 = u0 ? w2 : (le1 ? n0 : n1);
+    s0 = le1 ? w3 : (pop ? n1 : n0);
     // 2 pushes (used 0), 1 push (used 1), none (used 2), used - 2 pops: min(max(nsp + 2 - used, 0), 2)
     const uint32_t grown = nsp + 2u;
     nsp = min(grown > used ? grown - used : 0u, 2u);

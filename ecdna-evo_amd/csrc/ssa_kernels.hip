@@ -363,7 +363,7 @@ __global__ void __launch_bounds__(kStepperBlock) ssa_stepper(const StepperArgs a
         }
 
         // waiting time
-        const float tau = div_in_range(softlog_neg(w.x, logtab), a0);
+        const float tau = softlog_neg(w.x, logtab) * rcp_rn(a0);  // (draw mapping v8)
 
         uint64_t x = ch;
         if (ch == 1u) {
@@ -1165,7 +1165,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     const bool dmA = g1A & !g2A;
                     const bool cA = go & (e < a.max_iter) & (nm + npf < stop32) & !overA & (a0A > 0.0f) & (!g0A | dmA);
                     const uint32_t nmB = nm + (g0A ? 0u : 1u) - (dmA ? 1u : 0u);
-                    const float tauA = div_in_range(lga, a0A);
+                    const float tauA = lga * rcp_rn(a0A);
                     const double tB = t + (double)tauA;
                     const float t32B = t32 + tauA;
                     // event e + 1, from the state after e
@@ -1182,7 +1182,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                     const bool cB = cA & pair_ok & (e + 1u < a.max_iter) & (nmB + npf < stop32) & !overB & (a0B > 0.0f) &
                                     (!g0B | dmB);
                     const uint32_t nmC = nmB + (g0B ? 0u : 1u) - (dmB ? 1u : 0u);
-                    const float tauB = div_in_range(lg2, a0B);
+                    const float tauB = lg2 * rcp_rn(a0B);
                     // commit. An N- event consumes no stream word after w1, so its spare update pushes w2 and
                     // w3 onto the stack and leaves exactly those two (spares_update with used = 0).
                     sp0 = cB ? w2 : (cA ? wa.w : sp0);
@@ -1229,7 +1229,7 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
                             if (g0 & !dm) {  // an N+ event: the full event draws it
                                 go = false;
                             } else {
-                                const float tau2 = div_in_range(softlog_neg(w2.x, logtab), a02);
+                                const float tau2 = softlog_neg(w2.x, logtab) * rcp_rn(a02);
                                 spares_update(0u, w2.z, w2.w, sp0, sp1, nsp);
                                 nm = nm + (g0 ? 0u : 1u) - (dm ? 1u : 0u);
                                 n_dm += dm ? 1u : 0u;
@@ -1505,14 +1505,16 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
             }
             CYC_MARK(12);
             if (apply) {
-                const float tau = div_in_range(softlog_neg(w.x, logtab), a0);
+                const float tau = softlog_neg(w.x, logtab) * rcp_rn(a0);  // (draw mapping v8)
                 CYC_MARK(13);
                 // common case: every copy number involved is binned -> LDS only, no branch
                 // (bin_add_ev clamps its copy number into range, so lanes adding 0 need no select)
-                bin_add_ev(k, (nplus_ev && small) ? 0xffffffffu : 0u);
-                bin_add_ev(da, sa ? 1u : 0u);
-                bin_add_ev(db, sb ? 1u : 0u);
-                ns = ns - ((nplus_ev && small) ? 1u : 0u) + (sa ? 1u : 0u) + (sb ? 1u : 0u);
+                // (the three deltas, 0 / +1 / -1 as u32 words, also update ns: one select each)
+                const uint32_t dk = (nplus_ev && small) ? 0xffffffffu : 0u, dda = sa ? 1u : 0u, ddb = sb ? 1u : 0u;
+                bin_add_ev(k, dk);
+                bin_add_ev(da, dda);
+                bin_add_ev(db, ddb);
+                ns = ns + dk + dda + ddb;
                 CYC_MARK(14);
                 spares_update(nplus_ev ? ws.pos : 0u, w.z, w.w, sp0, sp1, nsp);
                 nm = nm + ((!gA || (prolif && un == 1u)) ? 1u : 0u) - (death_nm ? 1u : 0u);

@@ -181,10 +181,9 @@ __global__ void __launch_bounds__(kRefBlock, ECDNA_REF_MIN_WAVES) ssa_stepper_re
         for (int c = 0; c < K; ++c) {
             const float lambda = rates[c] * (float)pop[c];
             if (!(lambda > 0.0f)) continue;
-            // 1 / lambda, the correctly rounded f32 quotient: div_in_range (ssa_device.hpp) is exact for a numerator in
-            // [2^-24, 16.7] and a divisor in [2^-60, 2^94], and lambda = rate * pop is in [2^-60, 2^92] (the ABI's rate
-            // range, u32 populations): the compiler's division without its scaling and fixup steps
-            const float inv = div_in_range(1.0f, lambda);
+            // 1 / lambda, the correctly rounded f32 quotient: rcp_rn (ssa_device.hpp) is RN32(1 / d) for every f32 d in
+            // [2^-60, 2^95), and lambda = rate * pop is in [2^-60, 2^92] (the ABI's rate range, u32 populations)
+            const float inv = rcp_rn(lambda);
             const float tau = (float)refdraws::exp1(rng, zx, zf, clog, cexp) * inv;
             if (ch < 0 || tau < best) {
                 best = tau;

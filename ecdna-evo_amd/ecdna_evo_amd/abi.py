@@ -14,9 +14,9 @@ from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 # the oldest library an A/B may load under ECDNA_SSA_ABI_ANY=1: the same Params layout as this ABI (v10 appended
-# max_workgroups; v11 changed no struct)
+# max_workgroups; v11 and v12 changed no struct)
 ABI_SAME_LAYOUT_SINCE = 10
 
 # ecdna_process_t (ProcessType, src/clap_app.rs:311-315)

@@ -43,12 +43,15 @@
 extern "C" {
 #endif
 
-/* ABI v11: ECDNA_REP_ERR_INTERNAL (a replicate whose event would pick from an empty N+ set stops instead of
+/* ABI v12: draw mapping v8, the time step as the soft log times the correctly rounded reciprocal RN32(1 / a0) (v7
+ * divided: the correctly rounded quotient; the two differ by at most one ulp, so results differ from v11's for the
+ * same seed). The Params layout and everything else are those of v11.
+ * ABI v11: ECDNA_REP_ERR_INTERNAL (a replicate whose event would pick from an empty N+ set stops instead of
  * indexing off its row); unknown flag bits are rejected; the lane-quad schedule (instance schedule 4) is gone.
- * The Params layout and draw mapping v7 are those of v10 (v10 appended ecdna_ssa_params_t.max_workgroups, a cap on
- * the persistent grid for contexts that share a GPU; v9 took the channel from all 32 bits of the event's word over
- * f64 cumulative propensities). */
-#define ECDNA_SSA_ABI_VERSION 11
+ * The Params layout is that of v10 (v10 appended ecdna_ssa_params_t.max_workgroups, a cap on the persistent grid for
+ * contexts that share a GPU; v9 took the channel from all 32 bits of the event's word over f64 cumulative
+ * propensities, draw mapping v7). */
+#define ECDNA_SSA_ABI_VERSION 12
 
 /* Process type — ProcessType (src/clap_app.rs:311-315); chosen as BirthDeath
  * when d0 > 0 or d1 > 0 (src/clap_app.rs:163-174, 194-200). */
@@ -95,7 +98,7 @@ typedef enum {
                                      bin store's large-k row would exceed big_cap */
     ECDNA_REP_ERR_REJECTION = 4,  /* BinomialNoUneven loop exceeded 4096 redraws (p < 2^-4096) */
     ECDNA_REP_ERR_INTERNAL = 5    /* an N+ event drawn with no N+ cell, or a cell index past n+ (ABI v11): the event
-                                     is not applied and the replicate stops. Unreachable under draw mapping v7 (a
+                                     is not applied and the replicate stops. Unreachable under draw mapping v8 (a
                                      zero-propensity channel is never drawn); the guard keeps a broken invariant
                                      from indexing off the row. The reference's pick_remove_random_nplus returns an
                                      error on an empty N+ set (src/proliferation.rs:57). */

@@ -26,9 +26,9 @@
  * Floating point: compile with -ffp-contract=off. Every f32 / f64 operation
  * below is a correctly rounded IEEE add/sub/mul/div/fma in a fixed order (the
  * propensities and time step in f32, the channel's cumulative sums and target
- * in f64, draw mapping v7; the clock in f64), so the HIP kernel (which spells
- * the same operations with contraction disabled) reproduces the times and
- * channel picks bit for bit.
+ * in f64, draw mapping v8: the time step a product with RN32(1 / a0); the
+ * clock in f64), so the HIP kernel (which spells the same operations with
+ * contraction disabled) reproduces the times and channel picks bit for bit.
  */
 #include "ssa_oracle.h"
 #include "ssa_logtab.h"
@@ -591,14 +591,17 @@ static void simulate_replicate(const ecdna_ssa_params_t* p, uint64_t rid, uint16
         /* direct method: channel by w1 against the cumulative propensities */
         const int ch = channel_of(c, chan_target(w[1], A));
         /* an N+ event with no N+ cell: the engine's guard (ECDNA_REP_ERR_INTERNAL, ABI v11). Unreachable under draw
-         * mapping v7 (a zero-propensity channel is never drawn); the reference's pick_remove_random_nplus errors on an
+         * mapping v8 (a zero-propensity channel is never drawn); the reference's pick_remove_random_nplus errors on an
          * empty N+ set (src/proliferation.rs:55-57). The event is not applied. */
         if ((ch & 1) && nplus == 0) {
             err = ECDNA_REP_ERR_INTERNAL;
             stop = ECDNA_STOP_ERROR;
             continue;
         }
-        float tau = oracle_softlog_neg(w[0]) / a0; /* the correctly rounded f32 quotient */
+        /* draw mapping v8: the soft log times the correctly rounded reciprocal RN32(1 / a0) (the f64 quotient rounded
+         * to f32: 1 / a0 is never within 2^-53 relative of an f32 rounding boundary, so the double rounding is
+         * innocuous); the engine forms RN32(1 / a0) from v_rcp_f32 and one Newton step (ssa_device.hpp rcp_rn) */
+        float tau = oracle_softlog_neg(w[0]) * (float)(1.0 / (double)a0);
         wstream ws;
         ws_init(&ws, p->seed, rid, e, w[2], w[3]);
         ws.sp[0] = spare[0];

@@ -6,10 +6,15 @@
 // "propensities" block): f32 products rate * f32(pop), f64 cumulative sums, then chan_target(w1, A) against the
 // boundaries. chan_target itself is the header's function, so a change of its scale or rounding that the oracle
 // does not share shows here, without a GPU.
-// Prints "cases=<n> mismatches=<m>" and exits 1 on any mismatch.
+// Then the time step's reciprocal (draw mapping v8): rcp_newton(d, r), the Newton step rcp_rn applies to the hardware's
+// v_rcp_f32, from both faithful starts r (RD and RU of 1 / d) against RN32(1 / d), for every d in [1, 2) and for
+// random d over [2^-60, 2^95): the step is exact from either start except from RD at mantissa 0x7fffff (1 / d within
+// 2^-49 of a rounding midpoint), where the GPU's rcp gives RU (tools/rcp_check.hip checks every d on the GPU).
+// Prints "rcp_cases=<n> rcp_off=<k>" and "cases=<n> mismatches=<m>"; exits 1 on any mismatch.
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <string.h>
 
 #include "ssa_device.hpp"
 
@@ -57,9 +62,46 @@ int kernel_channel(const float r[4], uint32_t nm, uint32_t np, bool bd, uint32_t
     return target < cA ? 0 : 1;
 }
 
+// RN32(1 / d): the f64 quotient rounded to f32 (1 / d is never within 2^-53 relative of an f32 rounding boundary)
+float rn_recip(float d) { return (float)(1.0 / (double)d); }
+
+// (cases, mismatches other than the known one) of rcp_newton from RD and RU of 1 / d
+void check_recip(float d, long& cases, long& bad, long& known) {
+    const double inv = 1.0 / (double)d;
+    const float yt = (float)inv;
+    const float rd = (double)yt <= inv ? yt : nextafterf(yt, 0.0f);
+    const float ru = (double)yt >= inv ? yt : nextafterf(yt, INFINITY);
+    for (const float r : {rd, ru}) {
+        ++cases;
+        if (ecdna::rcp_newton(d, r) == yt) continue;
+        uint32_t u;
+        memcpy(&u, &d, 4);
+        if ((u & 0x7fffffu) == 0x7fffffu && r == rd) {
+            ++known;
+            continue;
+        }
+        if (++bad <= 5) fprintf(stderr, "rcp mismatch: d %a r %a -> %a, RN %a\n", d, r, ecdna::rcp_newton(d, r), yt);
+    }
+}
+
 }  // namespace
 
 int main() {
+    long rc = 0, rbad = 0, rknown = 0;
+    for (uint32_t m = 0; m < (1u << 23); ++m) {
+        float d;
+        const uint32_t u = 0x3f800000u | m;
+        memcpy(&d, &u, 4);
+        check_recip(d, rc, rbad, rknown);
+    }
+    for (int i = 0; i < 2000000; ++i) {  // other binades: [2^-60, 2^95)
+        const uint64_t r = next_u64();
+        const uint32_t u = ((uint32_t)(67u + (r >> 32) % 155u) << 23) | (uint32_t)(r & 0x7fffffu);
+        float d;
+        memcpy(&d, &u, 4);
+        check_recip(d, rc, rbad, rknown);
+    }
+    printf("rcp_cases=%ld rcp_off=%ld rcp_known=%ld\n", rc, rbad, rknown);
     long cases = 0, bad = 0;
     for (int i = 0; i < 200000; ++i) {
         const float r[4] = {rand_rate(), rand_rate(), rand_rate(), rand_rate()};
@@ -95,6 +137,6 @@ int main() {
             }
         }
     }
-    printf("cases=%ld mismatches=%ld\n", cases, bad);
-    return bad ? 1 : 0;
+    printf("cases=%ld mismatches=%ld\n", cases, bad + rbad);
+    return (bad || rbad) ? 1 : 0;
 }

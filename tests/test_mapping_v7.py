@@ -1,4 +1,5 @@
-"""Draw mapping v7 on the CPU: the exact law of the channel pick and of the time draw.
+"""Draw mapping v7 / v8 on the CPU: the exact law of the channel pick and of the time draw (v8 = v7
+with the time step as a product with the correctly rounded reciprocal of a0).
 
 Channel (v7). The propensities are the reference's own f32 products rate_i * pop_i (src/main.rs:67, 139); their
 cumulative sums c_0 <= c_1 <= c_2 <= A are formed in f64, and the channel is the number of c_i <= target with
@@ -9,7 +10,8 @@ within 2^-32 (plus f64 rounding) of lambda_i / sum(lambda). The previous mapping
 f32 cumulative sums) is restated in numpy for contrast: it could not draw a channel below ~2^-24 of the
 total, and biased small ones (one N- cell among 1e6 N+ cells: -4.6 %; among 1e7: +19 %; among 1.7e7: never).
 
-Time draw (v6 = v7). tau = softlog(w0) / a0 with softlog(w0) = -ln u0, u0 = ((w0 >> 9) + 0.5) 2^-23,
+Time draw (v6 = v7 = v8). tau = softlog(w0) / a0 (v8: softlog(w0) * RN32(1 / a0), within one ulp of
+the quotient) with softlog(w0) = -ln u0, u0 = ((w0 >> 9) + 0.5) 2^-23,
 so the draw Exp(1) * a0 takes one of 2^23 values, each with probability 2^-23. All 2^23 soft-log values are enumerated
 through the oracle (the same f32 operations as the kernel) and compared with Exp(1): the KS distance, the mean, the
 second moment and the tail masses P(X > x). (The total variation distance between a discrete law and Exp(1) is 1 for
@@ -154,7 +156,8 @@ def test_kernel_header_channel_matches_the_oracle(tmp_path, oracle_mod):
     """The stepper header's chan_target (ecdna-evo_amd/csrc/ssa_device.hpp, host-callable) with the steppers'
     propensity sequence, compiled for the host and compared with oracle_channel over 1.7M cases: random rates in
     the accepted range (and zeros), populations 0 .. 2^32 - 1, and the words either side of every boundary
-    (tests/native/device_math_check.cpp). Guards the kernels' channel arithmetic on a machine without a GPU."""
+    (tests/native/device_math_check.cpp). Guards the kernels' channel arithmetic on a machine without a GPU. Then the
+    header's rcp_newton (the time step's reciprocal, draw mapping v8) against RN32(1 / d)."""
     exe = tmp_path / "device_math_check"
     subprocess.run(["hipcc", "-x", "hip", "--offload-host-only", "-std=c++17", "-O1", "-I",
                     os.path.join(REPO, "ecdna-evo_amd", "csrc"), os.path.join(REPO, "tests", "native",
@@ -164,11 +167,18 @@ def test_kernel_header_channel_matches_the_oracle(tmp_path, oracle_mod):
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
     assert out.stdout.strip().endswith("mismatches=0")
+    # the time step's reciprocal (draw mapping v8): the Newton step gives RN32(1 / d) from either faithful start, for
+    # every d of a binade and 2M random d over [2^-60, 2^95), except from RD at mantissa 0x7fffff (counted as known;
+    # the GPU's rcp is RU there: tools/rcp_check.hip, tests/test_gpu_rcp.py)
+    rcp = dict(kv.split("=") for kv in out.stdout.split("\n")[0].split())
+    assert int(rcp["rcp_cases"]) >= 2 * (2**23 + 2_000_000) and int(rcp["rcp_off"]) == 0, out.stdout
+    assert int(rcp["rcp_known"]) >= 1
 
 
 def test_time_step_operands_stay_normal():
-    """Soft log in [2^-24, 24 ln 2] over a0 = RN32(A) in [2^-60, 2^94]: quotient, reciprocal and the Newton residual
-    scale (n 2^-24) are all normal f32 numbers (>= 2^-126) and finite (the range condition of div_in_range)."""
+    """Soft log in [2^-24, 24 ln 2] times RN32(1 / a0), a0 = RN32(A) in [2^-60, 2^94] (draw mapping v8): the
+    reciprocal, the Newton residual and the product are all normal f32 numbers (>= 2^-126) and finite, the range over
+    which rcp_rn is RN32(1 / d) (checked for every f32 in [2^-60, 2^95) on the GPU)."""
     tiny = np.finfo(np.float32).tiny
     n_min, n_max = 2.0**-24, 24 * np.log(2.0)
     d_min, d_max = 2.0**-60, 2.0**94

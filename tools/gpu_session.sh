@@ -5,7 +5,7 @@
 #     parity     the parity subset only (parity, random parity, rotation, drain, rare channels)
 #     ab_c3      C3 (K = 32) with each prebuilt library of LIBS, interleaved twice (tools/ab_libs.sh)
 #     stall      two PMC passes per library of LIBS: the SQ wave-cycle split, LDS / branch / fetch counters
-#     rcp        the time step's reciprocal against RN32(1 / b) for every f32 b the stepper divides by (tools/rcp_check)
+#     rcp        the time step's reciprocal against RN32(1 / b) for every f32 b the stepper divides by (ecdna-evo_amd/bin/rcp_check, tools/rcp_check.hip)
 #     latency    C2, C4 rank-0 shard, C5 rank-0 shard with each library (tools/ab_latency.sh)
 #     pmc        one SQ-counter pass (VALU / SALU / LDS per wave-event of one C3 step) per library
 #     c3s        the C3 fixed-total shards (G = 1, 2, 4, 8; all ranks) with the working tree (tools/c3_strong.py)
@@ -64,7 +64,7 @@ for step in ${STEPS//,/ }; do
         python3 tools/ab_pmc_summary.py gpurun_out/${TAG}_pmc_$n gpurun_out/${TAG}_pmc_$n.log "$n" | tee -a gpurun_out/${TAG}_pmc.txt
       done ;;
     rcp)
-      rc=0; timeout -k 10 120 tools/rcp_check > gpurun_out/${TAG}_rcp_check.json || rc=$?
+      rc=0; timeout -k 10 120 ecdna-evo_amd/bin/rcp_check > gpurun_out/${TAG}_rcp_check.json || rc=$?
       cat gpurun_out/${TAG}_rcp_check.json; [ $rc -le 1 ] || exit 1 ;;  # (1: mismatches found, reported)
     stall)  # the SQ wave-cycle split (waiting on waitcnt / issue-stalled / issuing) and the LDS, branch and fetch counters
       for n in $LIBS; do
