@@ -1315,6 +1315,10 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
             const bool prolif = gA && !gB;
             const bool death_nm = gB && !gC;
             const bool nplus_ev = prolif || gC;  // ProliferateNPlus or DeathNPlus: a cell is picked
+            // the waiting time, formed here (it needs only w0 and a0): its soft-log table read and its chain of dependent
+            // f32 operations then share a basic block with the pick's, whose LDS round trips they fill in a lone wave
+            // (formed in the commit, behind the rare branch, it followed them)
+            const float tau = softlog_neg(w.x, logtab) * rcp_rn(a0);  // (draw mapping v8)
 
             CYC_MARK(9);
             WordStream ws;
@@ -1505,7 +1509,6 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
             }
             CYC_MARK(12);
             if (apply) {
-                const float tau = softlog_neg(w.x, logtab) * rcp_rn(a0);  // (draw mapping v8)
                 CYC_MARK(13);
                 // common case: every copy number involved is binned -> LDS only, no branch
                 // (bin_add_ev clamps its copy number into range, so lanes adding 0 need no select)

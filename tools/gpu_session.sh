@@ -5,6 +5,7 @@
 #     parity     the parity subset only (parity, random parity, rotation, drain, rare channels)
 #     ab_c3      C3 (K = 32) with each prebuilt library of LIBS, interleaved twice (tools/ab_libs.sh)
 #     stall      two PMC passes per library of LIBS: the SQ wave-cycle split, LDS / branch / fetch counters
+#                (STALL_ARGS: bench.py arguments, e.g. "--workload c2"; default the C3 line)
 #     rcp        the time step's reciprocal against RN32(1 / b) for every f32 b the stepper divides by (ecdna-evo_amd/bin/rcp_check, tools/rcp_check.hip)
 #     latency    C2, C4 rank-0 shard, C5 rank-0 shard with each library (tools/ab_latency.sh)
 #     pmc        one SQ-counter pass (VALU / SALU / LDS per wave-event of one C3 step) per library
@@ -70,10 +71,11 @@ for step in ${STEPS//,/ }; do
       for n in $LIBS; do
         k=0
         for pass in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS" \
-                    "SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_IFETCH SQ_ACTIVE_INST_MISC SQ_BUSY_CYCLES SQ_INSTS_SMEM SQ_WAVES"; do
+                    "SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_IFETCH SQ_ACTIVE_INST_MISC SQ_BUSY_CYCLES SQ_INSTS_SMEM SQ_WAVES" \
+                    "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_FLAT SQ_INST_CYCLES_SALU SQ_WAVES"; do
           k=$((k + 1))
           ECDNA_SSA_LIB=$L/$n/libecdna_ssa.so timeout -s KILL 300 rocprofv3 --pmc $pass -T --output-format csv \
-            -d gpurun_out/${TAG}_stall_${n}_$k -o pmc -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline \
+            -d gpurun_out/${TAG}_stall_${n}_$k -o pmc -- python3 bench.py ${STALL_ARGS:-} --steps 1 --warmup 0 --no-cpu-baseline \
             > gpurun_out/${TAG}_stall_${n}_$k.log 2>&1
           python3 tools/ab_pmc_summary.py gpurun_out/${TAG}_stall_${n}_$k gpurun_out/${TAG}_stall_${n}_$k.log "$n" all \
             | tee -a gpurun_out/${TAG}_stall.txt
