@@ -489,11 +489,18 @@ def main():
                 "measured_2cycle_class_per_s": two,
                 "measured_4cycle_class_per_s": four,
                 "frac_of_measured_4cycle_class": per_event * kernel_eps / four if four else None,
+                # scalar and LDS instructions take issue slots too (round 6: an added s_mov costs 0.6 of an added
+                # v_xor at C3, profiles/r06n_marginal_valu_salu.txt)
+                "salu_wave_insts_per_event": (pmc["salu_wave_insts_per_wave_event"] / 64.0
+                                              if "salu_wave_insts_per_wave_event" in pmc else None),
+                "lds_wave_insts_per_event": (pmc["lds_wave_insts_per_wave_event"] / 64.0
+                                             if "lds_wave_insts_per_wave_event" in pmc else None),
                 "note": "the bin store keeps every common-case event in LDS and registers, so the stepper is "
-                        "bounded by vector-instruction issue, not HBM (DESIGN.md §5); VALU wave-instructions per "
-                        "event from the committed PMC summary (SQ_INSTS_VALU); the spec peak assumes 2 cycles per "
-                        "wave64 instruction, which only the VOP2 logic/add/mov class reaches on gfx950 — most of "
-                        "the stepper's instructions are in the measured 4-cycle class (tools/valu_probe.hip)",
+                        "bounded by instruction issue, not HBM (DESIGN.md §5): vector instructions first, scalar "
+                        "control next; wave-instructions per event from the committed PMC summary (SQ_INSTS_VALU / "
+                        "_SALU / _LDS); the spec peak assumes 2 cycles per wave64 instruction, which only the VOP2 "
+                        "logic/add/mov class reaches on gfx950 — most of the stepper's instructions are in the "
+                        "measured 4-cycle class (tools/valu_probe.hip)",
             }
         if args.store == "rows" and "read_requests_per_event" in pmc:
             per_event = pmc["read_requests_per_event"] + pmc["write_requests_per_event"]
