@@ -1,8 +1,9 @@
 """SQ instruction counts per wave-event of the bin stepper from one rocprofv3 --pmc pass over a 1-step bench
 (tools/gpu_session.sh, step pmc). Development tool. Usage: python tools/ab_pmc_summary.py <pmc dir> <bench stdout> <name> [all]
 (all: every counter of the pass per wave-event, e.g. the SQ_WAIT_* / SQ_ACTIVE_* stall split of tools/gpu_session.sh's
-stall step)"""
+stall step; PMC_KERNEL: the kernel-name prefix summed, default ssa_stepper_bins)"""
 import csv
+import os
 import glob
 import json
 import sys
@@ -15,7 +16,7 @@ def main(pmc_dir, bench_log, name, every=""):
         return
     tot = {}
     for r in csv.DictReader(open(paths[0])):
-        if r["Kernel_Name"].startswith("ssa_stepper_bins"):
+        if r["Kernel_Name"].startswith(os.environ.get("PMC_KERNEL", "ssa_stepper_bins")):
             tot[r["Counter_Name"]] = tot.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
             tot["VGPR"] = int(r["VGPR_Count"])
     ev = None
