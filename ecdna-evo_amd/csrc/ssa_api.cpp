@@ -479,10 +479,8 @@ int ecdna_ssa_ctx_create(const ecdna_ssa_params_t* p, ecdna_ssa_ctx** out) {
         // u16 counters hold at most 65535 cells per bin/group; K = 32 always uses u32 counters: the same LDS
         // footprint as K = 64/u16 (144 B per lane), no 16-bit packing in the updates and the scan (C3:
         // 119 ms against 126 ms with u16)
-        // (ECDNA_SSA_C32 = 1 forces u32 counters at any K, = 0 u16 counters at K = 32 where cell_cap allows: a
-        // development knob, results are the same)
-        const uint64_t c32_knob = env_u64("ECDNA_SSA_C32", 2);
-        c->bin_c32 = (p->cell_cap > 65535u || c32_knob == 1 || (c->bin_k <= 32 && c32_knob != 0)) ? 1 : 0;
+        // (ECDNA_SSA_C32 = 1 forces u32 counters at any K: a development knob, results are the same)
+        c->bin_c32 = (p->cell_cap > 65535u || c->bin_k <= 32 || env_u64("ECDNA_SSA_C32", 0)) ? 1 : 0;
         c->stepper_block = (uint32_t)ecdna::bin_stepper_block(c->bin_k);
     }
     const uint64_t bag_bytes = (uint64_t)c->bin_k * (c->bin_c32 ? 4u : 2u);
