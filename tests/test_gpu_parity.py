@@ -280,3 +280,24 @@ def test_gpu_nminus_fast_forward_matches_oracle(name, engine_mod, oracle_mod, mo
     ev = s["events_by_type"].astype(np.int64)
     nminus_share = (ev[:, 0] + ev[:, 2]).sum() / ev.sum()
     assert nminus_share > 0.6, nminus_share  # the fast-forward's regime
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flags,kmax", [(0, 0), (abi.FLAG_BIN_STORE, 32), (abi.FLAG_BIN_STORE, 64)])
+def test_gpu_empty_replicates_stop_with_their_error_at_every_limit(flags, kmax, engine_mod, oracle_mod):
+    """An empty initial distribution stops with ECDNA_REP_ERR_EMPTY and ECDNA_STOP_ERROR whatever other limit would
+    hold at its first stop test (round 6: the bin stepper records the error at the claim and stops the replicate at
+    that iteration's stop test, whose reason follows the error), mixed with non-empty sets in one launch; bit for bit
+    against the oracle. max_iter 0 and a cell limit of 1 make every other stop condition true at the first test."""
+    for max_iter, max_cells in ((0, 100), (50, 1), (50, 100)):
+        spec = abi.RunSpec(seed=9, process=abi.BIRTH_DEATH, rates=((1.0, 1.5, 0.3, 0.3),) * 2, n_replicates=16,
+                           reps_per_set=8, max_cells=max_cells, max_iter=max_iter,
+                           init_per_set=[{}, {1: 2, 3: 1}], flags=abi.FLAG_EVENT_HASH | flags, bin_kmax=kmax)
+        gpu = engine_mod.run(spec, want_rows=True)
+        cpu = oracle_mod.run(spec, mode="philox", want_rows=True)
+        _compare(gpu, cpu, f"empty/{flags}/{kmax}/{max_iter}/{max_cells}")
+        s = gpu.summaries
+        empty = np.arange(16) < 8
+        assert (s["error"][empty] == abi.REP_ERR_EMPTY).all() and (s["stop_reason"][empty] == abi.STOP_ERROR).all()
+        assert (s["iters"][empty] == 0).all()
+        assert (s["error"][~empty] == 0).all()
