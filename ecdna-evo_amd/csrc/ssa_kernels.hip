@@ -1451,6 +1451,11 @@ __global__ void __launch_bounds__(BLK, SCH == 2 ? 4 : 1) ssa_stepper_bins(const 
             // (np == 0 gives idx 0). Unreachable under draw mapping v7; a broken channel would otherwise swap_remove
             // from an empty large-k row and wrap nb. Any event, death included; the oracle returns the same code.
             const bool internal = TF != 0 && nplus_ev && idx >= np;
+            // the waiting time held here, before the rare branch: left free, the compiler sank it into the commit, so
+            // its soft-log table load was still pending on the stop path and the loop top waited for every LDS operation
+            // of the wave (lgkmcnt(0): the previous event's six counter adds) before the propensities (C2 6.3-6.4 -> 6.1-6.3 ms,
+            // the C4 shard -2.5 %, C3 -0.4 %; profiles/r06ag_tau_pin_ab.txt)
+            asm volatile("" ::"v"(tau));
             // daughters (none for a death): [k1, k2] on an even split, [n] on an uneven one
             const uint32_t da = (un == 0u) ? k1v : n;
             const uint32_t db = n - k1v;
