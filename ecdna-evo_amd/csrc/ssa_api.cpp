@@ -783,7 +783,13 @@ int ecdna_ssa_ctx_launch(ecdna_ssa_ctx* c, void* stream) {
         // pass no faster at C3, 0.29 -> 0.30 ms, and C4's 1,024 sets 5 -> 28 ms, each workgroup walking more sets)
         const uint32_t hist_blocks_max = (uint32_t)c->cus * 8u;
         uint32_t rpb = (ch.n + hist_blocks_max - 1) / hist_blocks_max;
-        if (rpb < 4) rpb = 4;
+        // at least one replicate per lane of a workgroup, or the chunk's replicates of one parameter set if fewer: small
+        // runs otherwise spread over 2,048 workgroups of mostly idle waves, each adding its own nonzero bins to the
+        // same global words (C2: 0.061 -> 0.023 ms per launch at 256, 0.038 at 64, 0.052 at 1,024;
+        // profiles/r06ak_hist_rpb.txt); sweeps of small sets keep about one set per workgroup
+        const uint64_t set_local = std::max<uint64_t>(1, p.reps_per_set / stride);
+        const uint32_t rpb_min = (uint32_t)std::max<uint64_t>(4, std::min<uint64_t>(ecdna::kHistBlock, set_local));
+        if (rpb < rpb_min) rpb = rpb_min;
         hsa.reps_per_block = rpb;
         hsa.stats = c->d_stats ? c->d_stats + ch.first : nullptr;
         hsa.target_cdf = c->d_target_cdf;
